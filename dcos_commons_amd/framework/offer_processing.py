@@ -1,0 +1,470 @@
+"""The offer-processing loop and its helpers.
+
+Reference: sdk/.../framework/{OfferProcessor,OfferQueue,ReviveManager,TokenBucket,OfferAccepter,
+ImplicitReconciler}.java. Per cycle: take queued offers -> client status (revive / suppress /
+remove) -> client.offers -> unexpected-resource cleanup (DESTROY before UNRESERVE) -> decline ->
+ACCEPT (one call per agent, RESERVE/CREATE/.../LAUNCH_GROUP in order) -> revive if requested.
+
+MI355X-build changes (all opt-in knobs, reference behaviour is the default of each knob):
+* **event-driven wake-up** -- ``kick()`` (called on every status update) wakes the loop
+  immediately instead of waiting out the 5 s offer poll (OfferProcessor.java:46);
+* **bounded offer holding** -- while the service is WORKING, unused offers can be held for up to
+  ``hold_s`` and re-evaluated as plans advance instead of being declined for an hour and
+  re-obtained through a (rate-limited) REVIVE. ``hold_s=0`` is the reference behaviour.
+"""
+from __future__ import annotations
+
+import collections
+import logging
+import threading
+import time
+from typing import Callable, Dict, List, Optional
+
+from dcos_commons_amd import metrics
+from dcos_commons_amd.mesos import protos as P
+from dcos_commons_amd.offer import constants
+from dcos_commons_amd.offer.recommendations import DestroyOfferRecommendation, UnreserveOfferRecommendation
+from dcos_commons_amd.scheduler.mesos_event_client import (
+    ClientStatusResult,
+    IdleRequest,
+    OfferResult,
+    UnexpectedResult,
+)
+from dcos_commons_amd.storage.persister_utils import clear_all_data
+
+from . import driver
+from .process_exit import ProcessExit
+
+LOGGER = logging.getLogger(__name__)
+DEFAULT_OFFER_WAIT_S = 5.0
+DEFAULT_QUEUE_CAPACITY = 100
+ACCEPT_FILTERS = P.Filters(refuse_seconds=1)
+
+
+class OfferQueue:
+    def __init__(self, capacity: int = DEFAULT_QUEUE_CAPACITY):
+        self.capacity = capacity
+        self._q: collections.deque = collections.deque()
+        self._cond = threading.Condition()
+
+    def offer(self, o: P.Offer) -> bool:
+        with self._cond:
+            if self.capacity and len(self._q) >= self.capacity:
+                return False
+            self._q.append(o)
+            self._cond.notify_all()
+            return True
+
+    def take_all(self, wait_s: float, wake: Optional[threading.Event] = None) -> List[P.Offer]:
+        with self._cond:
+            if not self._q and wait_s > 0:
+                deadline = time.monotonic() + wait_s
+                while not self._q:
+                    if wake is not None and wake.is_set():
+                        break
+                    remaining = deadline - time.monotonic()
+                    if remaining <= 0:
+                        break
+                    self._cond.wait(min(remaining, 0.05) if wake is not None else remaining)
+            out = list(self._q)
+            self._q.clear()
+            return out
+
+    def notify(self) -> None:
+        with self._cond:
+            self._cond.notify_all()
+
+    def remove(self, offer_id: P.OfferID) -> bool:
+        with self._cond:
+            before = len(self._q)
+            self._q = collections.deque(o for o in self._q if o.id.value != offer_id.value)
+            return len(self._q) != before
+
+    def is_empty(self) -> bool:
+        with self._cond:
+            return not self._q
+
+    def size(self) -> int:
+        with self._cond:
+            return len(self._q)
+
+
+class TokenBucket:
+    """Revive rate limiter: capacity 256, +1 token every 256 s, >= 5 s between acquires."""
+
+    def __init__(self, initial: int = 256, capacity: int = 256, increment_interval_s: float = 256.0,
+                 acquire_interval_s: float = 5.0, clock: Callable[[], float] = time.monotonic):
+        if initial < 0 or capacity < 1 or increment_interval_s <= 0 or acquire_interval_s < 0:
+            raise ValueError("TokenBucket construction failed with invalid configuration")
+        self.initial = initial
+        self.count = initial
+        self.capacity = capacity
+        self.increment_interval_s = increment_interval_s
+        self.acquire_interval_s = acquire_interval_s
+        self.clock = clock
+        self._last_acquire: Optional[float] = None
+        self._last_increment = clock()
+        self._lock = threading.Lock()
+
+    def _refill(self) -> None:
+        now = self.clock()
+        n = int((now - self._last_increment) // self.increment_interval_s)
+        if n > 0:
+            self.count = min(self.capacity, self.count + n)
+            self._last_increment += n * self.increment_interval_s
+
+    def try_acquire(self) -> bool:
+        with self._lock:
+            self._refill()
+            now = self.clock()
+            if self.count > 0 and (self._last_acquire is None or now - self._last_acquire >= self.acquire_interval_s):
+                self.count -= 1
+                self._last_acquire = now
+                return True
+            return False
+
+    def reset(self) -> None:
+        with self._lock:
+            self.count = self.initial
+            self._last_acquire = None
+
+
+class ReviveManager:
+    def __init__(self, token_bucket: TokenBucket, suppress_enabled: bool = True):
+        self.bucket = token_bucket
+        self.suppress_enabled = suppress_enabled
+        self.revive_requested = False
+        self.is_suppressed = False
+
+    def notify_offers_received(self) -> None:
+        self.is_suppressed = False
+        metrics.not_suppressed()
+
+    def suppress_if_active(self) -> None:
+        if self.is_suppressed:
+            return
+        if self.suppress_enabled:
+            d = driver.get_instance()
+            if d is not None:
+                d.suppress_offers()
+            metrics.increment_suppresses()
+        self.is_suppressed = True
+
+    def request_revive_if_suppressed(self) -> None:
+        if self.is_suppressed:
+            self.request_revive()
+
+    def request_revive(self) -> None:
+        self.revive_requested = True
+
+    def revive_if_requested(self) -> None:
+        if not self.revive_requested:
+            return
+        if not self.bucket.try_acquire():
+            metrics.increment_revive_throttles()
+            return
+        d = driver.get_instance()
+        if d is not None:
+            d.revive_offers()
+        self.revive_requested = False
+        metrics.increment_revives()
+
+
+class OfferAccepter:
+    """Groups operations per agent (keeping op order) and issues one ACCEPT per agent."""
+
+    @staticmethod
+    def group_by_agent(recs) -> Dict[str, list]:
+        out: Dict[str, list] = {}
+        for r in recs:
+            out.setdefault(r.agent_id.value, []).append(r)
+        return dict(sorted(out.items()))
+
+    def accept(self, recs) -> None:
+        if not recs:
+            return
+        d = driver.get_instance()
+        for agent, agent_recs in self.group_by_agent(recs).items():
+            ops, offer_ids, seen = [], [], set()
+            for r in agent_recs:
+                op = r.get_operation()
+                if op is None:
+                    continue
+                ops.append(op)
+                if r.offer_id.value not in seen:
+                    seen.add(r.offer_id.value)
+                    offer_ids.append(r.offer_id)
+            if not ops:
+                continue
+            LOGGER.info("Sending %d operation(s) for agent %s: %s", len(ops), agent,
+                        [P.Offer.Operation.Type.Name(o.type) for o in ops])
+            d.accept_offers(offer_ids, ops, ACCEPT_FILTERS)
+
+
+def filter_out_accepted(offers, recs) -> List[P.Offer]:
+    used = {r.offer_id.value for r in recs if r.get_operation() is not None}
+    return [o for o in offers if o.id.value not in used]
+
+
+def to_cleanup_recommendations(offer_resources_list) -> list:
+    destroys, unreserves = [], []
+    for orr in offer_resources_list:
+        for r in orr.resources:
+            if r.HasField("disk") and r.disk.HasField("persistence"):
+                destroys.append(DestroyOfferRecommendation(orr.offer, r))
+            unreserves.append(UnreserveOfferRecommendation(orr.offer, r))
+    return destroys + unreserves
+
+
+def decline(offers, refuse_seconds: float) -> None:
+    d = driver.get_instance()
+    f = P.Filters(refuse_seconds=refuse_seconds)
+    for o in offers:
+        d.decline_offer(o.id, f)
+
+
+def decline_short(offers) -> None:
+    if offers:
+        decline(offers, constants.SHORT_DECLINE_SECONDS)
+        metrics.increment_declines_short(len(offers))
+
+
+def decline_long(offers) -> None:
+    if offers:
+        decline(offers, constants.LONG_DECLINE_SECONDS)
+        metrics.increment_declines_long(len(offers))
+
+
+class OfferProcessor:
+    def __init__(self, client, persister, scheduler_config=None, token_bucket: Optional[TokenBucket] = None,
+                 queue_capacity: int = DEFAULT_QUEUE_CAPACITY, offer_wait_s: Optional[float] = None,
+                 hold_s: float = 0.0, event_driven: bool = False):
+        self.client = client
+        self.persister = persister
+        self.offer_wait_s = offer_wait_s if offer_wait_s is not None else (
+            scheduler_config.offer_wait_s() if scheduler_config is not None else DEFAULT_OFFER_WAIT_S)
+        suppress = scheduler_config.is_suppress_enabled() if scheduler_config is not None else True
+        self.revive_manager = ReviveManager(token_bucket or TokenBucket(), suppress)
+        self.queue = OfferQueue(queue_capacity)
+        self.accepter = OfferAccepter()
+        self.multithreaded = True
+        self.hold_s = hold_s
+        self.event_driven = event_driven
+        self._held: Dict[str, tuple] = {}  # offer id -> (offer, hold deadline)
+        self._initialized = False
+        self._deregistered = False
+        self._in_progress = set()
+        self._in_progress_lock = threading.Lock()
+        self._wake = threading.Event()
+        self._stop = threading.Event()
+        self._thread: Optional[threading.Thread] = None
+        self.cycles = 0
+
+    def disable_threading(self) -> "OfferProcessor":
+        self.multithreaded = False
+        return self
+
+    def set_revive_token_bucket(self, bucket: TokenBucket) -> "OfferProcessor":
+        self.revive_manager.bucket = bucket
+        return self
+
+    def start(self) -> None:
+        if self.multithreaded and self._thread is None:
+            self._thread = threading.Thread(target=self._loop, name="OfferProcessor", daemon=True)
+            self._thread.start()
+        self._initialized = True
+
+    def stop(self) -> None:
+        self._stop.set()
+        self._wake.set()
+        self.queue.notify()
+        if self._thread is not None:
+            self._thread.join(timeout=5)
+
+    def _loop(self) -> None:
+        while not self._stop.is_set():
+            try:
+                self.process_queued_offers(self.offer_wait_s)
+            except Exception as e:  # noqa: BLE001
+                LOGGER.exception("Error encountered when processing offers, exiting to avoid zombie state")
+                ProcessExit.exit(ProcessExit.ERROR, e)
+                return
+
+    def kick(self) -> None:
+        """Wake the loop now (status update / plan change) instead of at the next offer poll."""
+        if self.event_driven:
+            self._wake.set()
+            self.queue.notify()
+
+    def enqueue(self, offers) -> None:
+        with self._in_progress_lock:
+            self._in_progress.update(o.id.value for o in offers)
+        for o in offers:
+            if not self.queue.offer(o):
+                LOGGER.warning("Offer queue is full: Declining offer and removing from in progress: '%s'", o.id.value)
+                decline_short([o])
+                with self._in_progress_lock:
+                    self._in_progress.discard(o.id.value)
+        if not self.multithreaded:
+            self.process_queued_offers(0)
+
+    def dequeue(self, offer_id: P.OfferID) -> None:
+        self.queue.remove(offer_id)
+        self._held.pop(offer_id.value, None)
+
+    def await_offers_processed(self, timeout_s: float = 5.0) -> None:
+        deadline = time.monotonic() + timeout_s
+        while time.monotonic() < deadline:
+            with self._in_progress_lock:
+                if not self._in_progress:
+                    return
+            time.sleep(0.01)
+        raise TimeoutError("Timed out waiting for offers to be processed")
+
+    def process_queued_offers(self, wait_s: float) -> None:
+        self._wake.clear()
+        new_offers = self.queue.take_all(wait_s, self._wake if self.event_driven else None)
+        if self._stop.is_set():
+            return
+        now = time.monotonic()
+        held = [o for o, _ in self._held.values()]
+        offers = held + new_offers
+        self.cycles += 1
+        try:
+            if new_offers:
+                self.revive_manager.notify_offers_received()
+            if not offers and not self._initialized:
+                return
+            if self._deregistered:
+                return
+            with metrics.process_offers_timer():
+                if self._check_status():
+                    self._evaluate(offers, now)
+                elif offers:
+                    self._held.clear()
+                    decline_long(offers)
+            self.revive_manager.revive_if_requested()
+        finally:
+            metrics.increment_processed_offers(len(new_offers))
+            with self._in_progress_lock:
+                for o in new_offers:
+                    self._in_progress.discard(o.id.value)
+
+    def _check_status(self) -> bool:
+        resp = self.client.get_client_status()
+        if resp.result == ClientStatusResult.WORKING:
+            if resp.has_new_work:
+                self.revive_manager.request_revive()
+            else:
+                self.revive_manager.request_revive_if_suppressed()
+            return True
+        if resp.idle_request == IdleRequest.NONE:
+            self.revive_manager.suppress_if_active()
+        elif resp.idle_request == IdleRequest.REMOVE_CLIENT:
+            self._deregistered = True
+            self._destroy_framework()
+        elif resp.idle_request == IdleRequest.START_UNINSTALL:
+            raise RuntimeError("Got unsupported START_UNINSTALL response. This should have been handled by a "
+                               "MultiServiceEventClient")
+        return False
+
+    def _evaluate(self, offers, now: float) -> None:
+        resp = self.client.offers(offers)
+        unused = filter_out_accepted(offers, resp.recommendations)
+        cleanup_result = UnexpectedResult.PROCESSED
+        cleanup_recs = []
+        if unused:
+            un = self.client.get_unexpected_resources(unused)
+            cleanup_result = un.result
+            cleanup_recs = to_cleanup_recommendations(un.offer_resources)
+        unused = filter_out_accepted(unused, cleanup_recs)
+        used = {o.id.value for o in offers} - {o.id.value for o in unused}
+        for oid in used:
+            self._held.pop(oid, None)
+        if unused:
+            if resp.result == OfferResult.PROCESSED and cleanup_result == UnexpectedResult.PROCESSED:
+                if self.hold_s > 0:
+                    to_decline = []
+                    for o in unused:
+                        prev = self._held.get(o.id.value)
+                        deadline = prev[1] if prev is not None else now + self.hold_s
+                        if deadline <= now:
+                            self._held.pop(o.id.value, None)
+                            to_decline.append(o)
+                        else:
+                            self._held[o.id.value] = (o, deadline)
+                    decline_short(to_decline)
+                else:
+                    decline_long(unused)
+            else:
+                for o in unused:
+                    self._held.pop(o.id.value, None)
+                decline_short(unused)
+        all_recs = list(resp.recommendations) + cleanup_recs
+        metrics.increment_recommendations(all_recs)
+        self.accepter.accept(all_recs)
+
+    def release_held(self) -> None:
+        """Decline every held offer (e.g. when the scheduler goes idle or stops)."""
+        held = [o for o, _ in self._held.values()]
+        self._held.clear()
+        decline_short(held)
+
+    def _destroy_framework(self) -> None:
+        try:
+            clear_all_data(self.persister)
+        except Exception as e:  # noqa: BLE001
+            raise RuntimeError("Failed to delete all persister data") from e
+        d = driver.get_instance()
+        if d is not None:
+            d.teardown()
+            d.stop(False)
+        self.client.unregistered()
+
+
+class ImplicitReconciler:
+    """Periodic ``reconcileTasks([])`` (delay 0, period 1 h by default)."""
+
+    def __init__(self, delay_s: float = 0.0, period_s: float = 3600.0):
+        self.delay_s = delay_s
+        self.period_s = period_s
+        self.multithreaded = True
+        self.started = False
+        self._stop = threading.Event()
+        self._thread = None
+
+    def disable_threading(self) -> "ImplicitReconciler":
+        self.multithreaded = False
+        return self
+
+    @staticmethod
+    def _reconcile() -> None:
+        try:
+            d = driver.get_instance()
+            if d is not None:
+                d.reconcile_tasks([])
+        except Exception:  # noqa: BLE001
+            LOGGER.exception("Failed to trigger implicit reconciliation")
+
+    def start(self) -> None:
+        if self.started:
+            raise RuntimeError("Start was already called")
+        self.started = True
+        if not self.multithreaded:
+            self._reconcile()
+            return
+
+        def loop():
+            if self._stop.wait(self.delay_s):
+                return
+            while True:
+                self._reconcile()
+                if self._stop.wait(self.period_s):
+                    return
+
+        self._thread = threading.Thread(target=loop, name="ImplicitReconciler", daemon=True)
+        self._thread.start()
+
+    def stop(self) -> None:
+        self._stop.set()
+        self.started = False

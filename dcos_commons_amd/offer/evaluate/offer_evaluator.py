@@ -1,0 +1,297 @@
+"""The core offer matcher.
+
+Reference: sdk/.../offer/evaluate/OfferEvaluator.java:65-857. For one ``PodInstanceRequirement``
+it builds the stage pipeline once -- *new* (first launch / permanent replace: placement, fresh
+reservations) or *existing* (relaunch in place on the pod's reservations, reusing a live executor)
+-- then runs it against each offer with a fresh ``MesosResourcePool`` and ``PodInfoBuilder``, and
+returns the recommendations of the first offer that passes every stage.
+
+MI355X-first notes: the evaluator is the CPU hot loop of the scheduler (the reference has no
+numeric kernels). ``evaluate`` reads the StateStore once per call (not per offer), and callers may
+pass a pre-fetched task map (``all_tasks``) so a whole offer cycle touches storage once.
+"""
+from __future__ import annotations
+
+import logging
+from typing import Dict, List, Optional, Sequence
+
+from dcos_commons_amd.mesos import protos as P
+from dcos_commons_amd.offer import task_utils
+from dcos_commons_amd.offer.history import OfferOutcome, OfferOutcomeTracker, OfferOutcomeTrackerV2
+from dcos_commons_amd.offer.resource_pool import MesosResourcePool
+from dcos_commons_amd.offer.resources import get_resource_id
+from dcos_commons_amd.offer.taskdata.labels import TaskException, TaskLabelReader
+from dcos_commons_amd.scheduler.plan.pod_instance_requirement import PodInstanceRequirement, RecoveryType
+from dcos_commons_amd.specification.specs import GoalState, NamedVIPSpec, PortSpec, ResourceSpec
+
+from .pod_info_builder import PodInfoBuilder
+from .resource_mappers import ExecutorResourceMapper, TaskResourceMapper
+from .stages import (
+    DestroyEvaluationStage,
+    ExecutorEvaluationStage,
+    LaunchEvaluationStage,
+    NamedVIPEvaluationStage,
+    PlacementRuleEvaluationStage,
+    PortEvaluationStage,
+    ResourceEvaluationStage,
+    UnreserveEvaluationStage,
+    VolumeEvaluationStage,
+    get_role,
+)
+
+
+def _ordered_resource_specs(resource_set) -> List[ResourceSpec]:
+    static_ports, dynamic_ports, simple = [], [], []
+    for r in resource_set.resources:
+        if isinstance(r, PortSpec):
+            (dynamic_ports if r.port == 0 else static_ports).append(r)
+        else:
+            simple.append(r)
+    return static_ports + dynamic_ports + simple
+
+
+def _executor_resource_specs(scheduler_config, role: str, principal: str, pre_reserved_role: str):
+    return [ResourceSpec(name=name, value=value, role=role, principal=principal, pre_reserved_role=pre_reserved_role)
+            for name, value in sorted(scheduler_config.executor_resources().items())]
+
+
+def _outcome_lines(outcome, indent: str = "") -> List[str]:
+    lines = [f"  {indent}{outcome}"]
+    for c in outcome.children:
+        lines.extend(_outcome_lines(c, indent + "  "))
+    return lines
+
+
+def _outcome_reasons(out: List[str], outcome) -> None:
+    out.append(f"{'PASS' if outcome.passing else 'FAIL'}({outcome.source}):{outcome.reason}")
+    for c in outcome.children:
+        _outcome_reasons(out, c)
+
+
+class OfferEvaluator:
+    def __init__(self, framework_store, state_store, service_name: str, target_config_id, template_url_factory,
+                 scheduler_config, resource_namespace: Optional[str] = None,
+                 offer_outcome_tracker: Optional[OfferOutcomeTracker] = None,
+                 offer_outcome_tracker_v2: Optional[OfferOutcomeTrackerV2] = None, tls_stage_factory=None):
+        self.framework_store = framework_store
+        self.state_store = state_store
+        self.service_name = service_name
+        self.target_config_id = target_config_id
+        self.template_url_factory = template_url_factory
+        self.scheduler_config = scheduler_config
+        self.resource_namespace = resource_namespace
+        self.offer_outcome_tracker = offer_outcome_tracker
+        self.offer_outcome_tracker_v2 = offer_outcome_tracker_v2
+        self.tls_stage_factory = tls_stage_factory
+        self._framework_id: Optional[str] = None
+        self.logger = logging.getLogger(__name__ + (f"({resource_namespace})" if resource_namespace else ""))
+
+    def _fid(self) -> P.FrameworkID:
+        fid = self.framework_store.fetch_framework_id()
+        if fid is None:
+            raise RuntimeError("FrameworkID is not yet stored; cannot evaluate offers before registration")
+        return fid
+
+    def evaluate(self, requirement: PodInstanceRequirement, offers: Sequence[P.Offer],
+                 all_tasks: Optional[Dict[str, P.TaskInfo]] = None) -> list:
+        fid_proto = self._fid()
+        if self._framework_id is None:
+            self._framework_id = fid_proto.value
+        if all_tasks is None:
+            all_tasks = {t.name: t for t in self.state_store.fetch_tasks()}
+        pi = requirement.pod_instance
+        this_pod = {}
+        for name in task_utils.get_task_names(pi):
+            t = all_tasks.get(name)
+            if t is not None:
+                this_pod[name] = t
+        stages = self.get_evaluation_pipeline(requirement, list(all_tasks.values()), this_pod)
+        role = get_role(pi.pod)
+        override_map = {ts.name: self.state_store.fetch_goal_override_status(f"{pi.name}-{ts.name}").target
+                        for ts in pi.pod.tasks}
+        target_config = self.get_target_config(requirement, this_pod)
+        for i, offer in enumerate(offers):
+            pool = MesosResourcePool(offer, role)
+            builder = PodInfoBuilder(requirement, self.service_name, target_config, self.template_url_factory,
+                                     self.scheduler_config, this_pod.values(), fid_proto, override_map)
+            outcomes = []
+            failed = 0
+            for stage in stages:
+                o = stage.evaluate(pool, builder)
+                outcomes.append(o)
+                if not o.passing:
+                    failed += 1
+            details_lines: List[str] = []
+            for o in outcomes:
+                details_lines.extend(_outcome_lines(o))
+            details = "\n".join(details_lines)
+            if failed:
+                self.logger.info("Offer %d, %s: failed %d of %d evaluation stages for %s:\n%s", i + 1,
+                                 offer.id.value, failed, len(stages), requirement.name, details)
+                self._track(requirement, False, offer, details, outcomes)
+                continue
+            recs = [r for o in outcomes for r in o.get_offer_recommendations()]
+            self.logger.info("Offer %d: passed all %d evaluation stages, returning %d recommendations for %s",
+                             i + 1, len(stages), len(recs), requirement.name)
+            self._track(requirement, True, offer, details, outcomes)
+            return recs
+        return []
+
+    def _track(self, requirement, passed, offer, details, outcomes) -> None:
+        if self.offer_outcome_tracker is not None:
+            self.offer_outcome_tracker.track(OfferOutcome(requirement.name, passed, offer, details))
+        if self.offer_outcome_tracker_v2 is not None:
+            reasons: List[str] = []
+            for o in outcomes:
+                _outcome_reasons(reasons, o)
+            s = self.offer_outcome_tracker_v2.summary
+            s.add_offer(OfferOutcome(requirement.name, passed, offer, reasons))
+            if not passed:
+                s.add_failure_agent(offer.agent_id.value)
+                for o in outcomes:
+                    if not o.passing:
+                        s.add_failure_reason(o.source)
+
+    # -- pipelines ---------------------------------------------------------------------
+    def get_evaluation_pipeline(self, requirement: PodInstanceRequirement, all_tasks, this_pod: Dict[str, P.TaskInfo]):
+        ids = [get_resource_id(r) for t in this_pod.values() for r in t.resources]
+        no_launched = all((i or "") == "" for i in ids if i is not None)
+        all_perm_failed = bool(this_pod) and all(TaskLabelReader(t).is_permanently_failed()
+                                                 for t in this_pod.values())
+        if requirement.recovery_type == RecoveryType.PERMANENT or all_perm_failed:
+            new = True
+        elif no_launched:
+            new = True
+        else:
+            new = False
+        pod = requirement.pod_instance.pod
+        tls = self.tls_stage_factory if any(t.transport_encryption for t in pod.tasks) else None
+        if new:
+            return self._new_pipeline(requirement, all_tasks, tls)
+        executor_info = self._executor_info(requirement, this_pod)
+        eid = executor_info.executor_id if executor_info.executor_id.value else None
+        return [ExecutorEvaluationStage(self.service_name, eid)] + \
+            self._existing_pipeline(requirement, this_pod, all_tasks, executor_info, tls)
+
+    def _executor_info(self, requirement, this_pod: Dict[str, P.TaskInfo]) -> P.ExecutorInfo:
+        names = task_utils.get_task_names(requirement.pod_instance, requirement.tasks_to_launch)
+        for t in this_pod.values():
+            if t.name in names:
+                continue
+            if self._has_reusable_executor(t):
+                return t.executor
+        first = next(iter(this_pod.values()))
+        e = P.ExecutorInfo()
+        e.CopyFrom(first.executor)
+        e.executor_id.value = ""
+        return e
+
+    def _has_reusable_executor(self, t: P.TaskInfo) -> bool:
+        status = self.state_store.fetch_status(t.name)
+        if status is None or TaskLabelReader(t).is_permanently_failed():
+            return False
+        return status.state in (P.TASK_STAGING, P.TASK_STARTING, P.TASK_RUNNING)
+
+    def _new_pipeline(self, requirement, all_tasks, tls):
+        pi = requirement.pod_instance
+        pod = pi.pod
+        ns, fid = self.resource_namespace, self._framework_id
+        stages = [ExecutorEvaluationStage(self.service_name, None)]
+        if pod.placement_rule is not None:
+            stages.append(PlacementRuleEvaluationStage(all_tasks, pod.placement_rule))
+        for v in pod.volumes:
+            stages.append(VolumeEvaluationStage.get_new(v, [], ns, fid))
+        if tls is not None:
+            for ts in pod.tasks:
+                if ts.transport_encryption:
+                    stages.append(tls(ts.name))
+        rs_by_task = {ts.name: ts.resource_set for ts in sorted(pod.tasks, key=lambda t: t.name)}
+        added_executor = False
+        added_sets = set()
+        for task_name, rs in rs_by_task.items():
+            specs = _ordered_resource_specs(rs)
+            if not added_executor:
+                added_executor = True
+                for spec in _executor_resource_specs(self.scheduler_config, specs[0].role, specs[0].principal,
+                                                     specs[0].pre_reserved_role):
+                    stages.append(ResourceEvaluationStage(spec, [], None, ns, fid))
+            if rs.id not in added_sets:
+                names = sorted(n for n, r in rs_by_task.items() if r.id == rs.id)
+                added_sets.add(rs.id)
+                for spec in specs:
+                    if isinstance(spec, NamedVIPSpec):
+                        stages.append(NamedVIPEvaluationStage(spec, names, None, ns, fid))
+                    elif isinstance(spec, PortSpec):
+                        stages.append(PortEvaluationStage(spec, names, None, ns, fid))
+                    else:
+                        stages.append(ResourceEvaluationStage(spec, names, None, ns, fid))
+                for v in rs.volumes:
+                    stages.append(VolumeEvaluationStage.get_new(v, names, ns, fid))
+            stages.append(LaunchEvaluationStage(self.service_name, task_name,
+                                                task_name in requirement.tasks_to_launch))
+        return stages
+
+    def _existing_pipeline(self, requirement, this_pod, all_tasks, executor_info, tls):
+        pi = requirement.pod_instance
+        pod = pi.pod
+        ns, fid = self.resource_namespace, self._framework_id
+        stages = []
+        if tls is not None:
+            for ts in pod.tasks:
+                if ts.transport_encryption:
+                    stages.append(tls(ts.name))
+        if pod.placement_rule is not None and requirement.recovery_type == RecoveryType.PERMANENT:
+            stages.append(PlacementRuleEvaluationStage(all_tasks, pod.placement_rule))
+        first_spec = next(r for ts in pod.tasks for r in ts.resource_set.resources)
+        mapper = ExecutorResourceMapper(
+            pod, _executor_resource_specs(self.scheduler_config, first_spec.role, first_spec.principal,
+                                          first_spec.pre_reserved_role),
+            executor_info.resources, ns, fid)
+        for r in mapper.orphaned_resources:
+            stages.append(DestroyEvaluationStage(r))
+        for r in mapper.orphaned_resources:
+            stages.append(UnreserveEvaluationStage(r))
+        stages.extend(mapper.evaluation_stages)
+        rs_by_task = {ts.name: ts.resource_set for ts in sorted(pod.tasks, key=lambda t: t.name)}
+        updated = set()
+        for task_name in requirement.tasks_to_launch:
+            rs = rs_by_task.get(task_name)
+            if rs is None:
+                raise ValueError(f"Unable to find task to launch {task_name} among defined tasks "
+                                 f"{list(rs_by_task)} in pod {requirement.name}. Malformed ServiceSpec?")
+            if rs.id in updated:
+                continue
+            updated.add(rs.id)
+            names_in_set = sorted(n for n, r in rs_by_task.items() if r.id == rs.id)
+            infos = [this_pod.get(f"{pi.name}-{n}") for n in names_in_set]
+            info = next((x for x in infos if x is not None), None)
+            if info is not None:
+                tm = TaskResourceMapper(names_in_set, rs, info, ns, fid)
+                for r in tm.orphaned_resources:
+                    stages.append(UnreserveEvaluationStage(r))
+                stages.extend(tm.evaluation_stages)
+            for n in names_in_set:
+                stages.append(LaunchEvaluationStage(self.service_name, n, n in requirement.tasks_to_launch))
+        return stages
+
+    def get_target_config(self, requirement: PodInstanceRequirement, this_pod: Dict[str, P.TaskInfo]):
+        if requirement.recovery_type == RecoveryType.NONE:
+            return self.target_config_id
+        running, other = {}, {}
+        pi = requirement.pod_instance
+        for ts in pi.pod.tasks:
+            if ts.name not in requirement.tasks_to_launch:
+                continue
+            name = f"{pi.name}-{ts.name}"
+            info = this_pod.get(name)
+            if info is None:
+                continue
+            try:
+                target = TaskLabelReader(info).get_target_configuration()
+            except (TaskException, ValueError):
+                continue
+            (running if ts.goal == GoalState.RUNNING else other)[name] = target
+        for m in (running, other):
+            if m:
+                return next(iter(m.values()))
+        return self.target_config_id

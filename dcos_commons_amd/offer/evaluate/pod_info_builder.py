@@ -1,0 +1,306 @@
+"""Builds the ``TaskInfo``/``ExecutorInfo`` protos for one pod instance.
+
+Reference: sdk/.../offer/evaluate/PodInfoBuilder.java:72-831. Stages mutate the builders held
+here; ``LaunchEvaluationStage`` snapshots them into launch / store recommendations.
+"""
+from __future__ import annotations
+
+import uuid
+from typing import Dict, List, Optional, Set
+
+from dcos_commons_amd.dcos import constants as dcos
+from dcos_commons_amd.http import endpoint_utils as eu
+from dcos_commons_amd.mesos import protos as P
+from dcos_commons_amd.offer import common_id_utils
+from dcos_commons_amd.offer import constants
+from dcos_commons_amd.offer.evaluate import placement
+from dcos_commons_amd.offer.resources import ResourceBuilder
+from dcos_commons_amd.offer.taskdata import labels as L
+from dcos_commons_amd.specification.specs import (
+    RLIMIT_INFINITY,
+    ConfigFileSpec,
+    PodInstance,
+    PodSpec,
+    ReadinessCheckSpec,
+    TaskSpec,
+    VolumeSpec,
+)
+from dcos_commons_amd.state.goal_state_override import PAUSE_READINESS_COMMAND, GoalStateOverride
+
+CONFIG_TEMPLATE_KEY_FORMAT = "CONFIG_TEMPLATE_%s"
+CONFIG_TEMPLATE_DOWNLOAD_PATH = "config-templates/"
+
+
+class InvalidRequirementException(Exception):
+    pass
+
+
+def get_task_environment(service_name: str, pod_instance: PodInstance, task_spec: TaskSpec,
+                         scheduler_config) -> Dict[str, str]:
+    env: Dict[str, str] = {}
+    if task_spec.command is not None:
+        env.update(task_spec.command.env)
+    task_name = f"{pod_instance.name}-{task_spec.name}"
+    env[L.POD_INSTANCE_INDEX_TASKENV] = str(pod_instance.index)
+    env[L.FRAMEWORK_NAME_TASKENV] = service_name
+    env[L.FRAMEWORK_HOST_TASKENV] = eu.to_auto_ip_domain(service_name, scheduler_config)
+    env[L.FRAMEWORK_VIP_HOST_TASKENV] = eu.to_vip_domain(service_name, scheduler_config)
+    env[L.SCHEDULER_API_HOSTNAME_TASKENV] = eu.to_scheduler_auto_ip_hostname(service_name, scheduler_config)
+    env[L.SCHEDULER_API_PORT_TASKENV] = str(scheduler_config.api_server_port())
+    env[L.TASK_NAME_TASKENV] = task_name
+    env[task_name] = "true"
+    env[L.PLACEMENT_REFERENCED_REGION_ENV] = str(placement.references_region(pod_instance.pod)).lower()
+    env[L.PLACEMENT_REFERENCED_ZONE_ENV] = str(placement.references_zone(pod_instance.pod)).lower()
+    return dict(sorted(env.items()))
+
+
+def config_template_download_path(config: ConfigFileSpec) -> str:
+    return CONFIG_TEMPLATE_DOWNLOAD_PATH + config.name
+
+
+def _reference_secret(path: str) -> P.Secret:
+    s = P.Secret(type=P.Secret.REFERENCE)
+    s.reference.name = path
+    return s
+
+
+class PodInfoBuilder:
+    def __init__(self, requirement, service_name: str, target_config_id, template_url_factory, scheduler_config,
+                 current_pod_tasks, framework_id: P.FrameworkID, override_map: Dict[str, GoalStateOverride]):
+        pi: PodInstance = requirement.pod_instance
+        self.pod_instance = pi
+        self.assigned_overlay_ports: Set[int] = set()
+        self.task_builders: Dict[str, P.TaskInfo] = {}
+        for ts in pi.pod.tasks:
+            self.task_builders[ts.name] = self._create_task_info(
+                pi, ts, requirement.environment, service_name, target_config_id, template_url_factory,
+                scheduler_config, override_map.get(ts.name, GoalStateOverride.NONE))
+            for rs in ts.resource_set.resources:
+                if rs.name == constants.PORTS_RESOURCE_TYPE and rs.value.ranges.range[0].begin > 0:
+                    self.assigned_overlay_ports.add(int(rs.value.ranges.range[0].begin))
+        self.executor_builder = self._executor_info(pi, framework_id, scheduler_config)
+        self.ports_by_task: Dict[str, Dict[str, int]] = {}
+        for t in current_pod_tasks:
+            if not L.TaskLabelReader(t).is_permanently_failed():
+                self.ports_by_task[t.name] = {p.name: int(p.number) for p in t.discovery.ports.ports if p.name}
+        for tb in self.task_builders.values():
+            self._validate(tb)
+
+    # -- accessors ---------------------------------------------------------------------
+    def get_task_builders(self) -> List[P.TaskInfo]:
+        return list(self.task_builders.values())
+
+    def get_task_builder(self, task_spec_name: str) -> P.TaskInfo:
+        return self.task_builders[task_spec_name]
+
+    def get_executor_builder(self) -> Optional[P.ExecutorInfo]:
+        return self.executor_builder
+
+    def get_prior_port_for_task(self, task_spec_name: str, port_spec) -> Optional[int]:
+        ports = self.ports_by_task.get(f"{self.pod_instance.name}-{task_spec_name}")
+        if ports is None:
+            return None
+        return ports.get(port_spec.port_name)
+
+    def get_task_resources(self) -> List[P.Resource]:
+        return [r for t in self.task_builders.values() for r in t.resources]
+
+    def get_executor_resources(self) -> List[P.Resource]:
+        return list(self.executor_builder.resources)
+
+    def is_assigned_overlay_port(self, port: int) -> bool:
+        return port in self.assigned_overlay_ports
+
+    def add_assigned_overlay_port(self, port: int) -> None:
+        self.assigned_overlay_ports.add(port)
+
+    @property
+    def type(self) -> str:
+        return self.pod_instance.pod.type
+
+    @property
+    def index(self) -> int:
+        return self.pod_instance.index
+
+    def set_executor_volume(self, volume_spec: VolumeSpec) -> None:
+        vol = P.Volume(mode=P.Volume.RW, container_path=volume_spec.container_path)
+        vol.source.type = P.Volume.Source.SANDBOX_PATH
+        vol.source.sandbox_path.type = P.Volume.Source.SandboxPath.PARENT
+        vol.source.sandbox_path.path = volume_spec.container_path
+        for t in self.task_builders.values():
+            t.container.type = P.ContainerInfo.MESOS
+            t.container.volumes.add().CopyFrom(vol)
+
+    @staticmethod
+    def get_existing_executor_volume(volume_spec, resource_id, resource_namespace, persistence_id, provider_id,
+                                     disk_source, framework_id) -> P.Resource:
+        return ResourceBuilder.from_volume_spec(volume_spec, resource_id, resource_namespace, persistence_id,
+                                                provider_id, disk_source, framework_id).build()
+
+    # -- construction ------------------------------------------------------------------
+    def _create_task_info(self, pi: PodInstance, ts: TaskSpec, environment: Dict[str, str], service_name: str,
+                          target_config_id, template_url_factory, scheduler_config,
+                          override: GoalStateOverride) -> P.TaskInfo:
+        pod = pi.pod
+        t = P.TaskInfo(name=f"{pi.name}-{ts.name}")
+        t.task_id.value = ""
+        t.agent_id.value = ""
+        w = L.TaskLabelWriter(t).set_target_configuration(target_config_id).set_type(pod.type).set_index(pi.index)
+        w.set_additional_labels(ts.labels)
+        w.apply()
+        if ts.command is not None:
+            cmd = t.command
+            cmd.environment.CopyFrom(L.env_from_map(get_task_environment(service_name, pi, ts, scheduler_config)))
+            if override == GoalStateOverride.PAUSED:
+                cmd.value = scheduler_config.pause_override_cmd()
+            else:
+                cmd.value = ts.command.value
+            for config in ts.config_files:
+                cmd.environment.CopyFrom(L.with_env_var(
+                    cmd.environment, CONFIG_TEMPLATE_KEY_FORMAT % L.to_env_name(config.name),
+                    f"{config_template_download_path(config)},{config.relative_path}"))
+            for k, v in environment.items():
+                cmd.environment.variables.add(name=k, value=v)
+            if override == GoalStateOverride.PAUSED:
+                cmd.uris.add(value=scheduler_config.bootstrap_uri())
+            for uri in pod.uris:
+                cmd.uris.add(value=uri)
+            for config in ts.config_files:
+                cmd.uris.add(value=template_url_factory(target_config_id, pod.type, ts.name, config.name),
+                             output_file=config_template_download_path(config), extract=False)
+            for secret in pod.secrets:
+                if secret.env_key is not None:
+                    v = cmd.environment.variables.add(name=secret.env_key, type=P.Environment.Variable.SECRET)
+                    v.secret.CopyFrom(_reference_secret(secret.secret_path))
+            if pod.user:
+                cmd.user = pod.user
+        if ts.discovery is not None:
+            d = t.discovery
+            if ts.discovery.prefix:
+                d.name = f"{ts.discovery.prefix}-{pi.index}"
+            d.visibility = (ts.discovery.visibility if ts.discovery.visibility is not None
+                            else constants.DEFAULT_TASK_DISCOVERY_VISIBILITY)
+        t.container.CopyFrom(self._container_info(pod, True, True))
+        if ts.shared_memory is not None:
+            t.container.linux_info.ipc_mode = P.LinuxInfo.IpcMode.Value(ts.shared_memory.value)
+        if ts.shared_memory_size is not None:
+            t.container.linux_info.shm_size = ts.shared_memory_size
+        self._set_health_check(t, service_name, pi, ts, override, scheduler_config)
+        self._set_readiness_check(t, service_name, pi, ts, override, scheduler_config)
+        if ts.kill_grace_period < 0:
+            raise InvalidRequirementException(
+                f"kill-grace-period must be zero or a positive integer, received: {ts.kill_grace_period}")
+        t.kill_policy.grace_period.nanoseconds = 1_000_000_000 * int(ts.kill_grace_period or 0)
+        return t
+
+    @staticmethod
+    def _set_health_check(t, service_name, pi, ts, override, scheduler_config) -> None:
+        hc = ts.health_check
+        if hc is None or override == GoalStateOverride.PAUSED:
+            return
+        h = t.health_check
+        h.delay_seconds = hc.delay
+        h.interval_seconds = hc.interval
+        h.timeout_seconds = hc.timeout
+        h.consecutive_failures = hc.max_consecutive_failures
+        h.grace_period_seconds = hc.grace_period
+        h.type = P.HealthCheck.COMMAND
+        h.command.value = hc.command
+        h.command.environment.CopyFrom(L.env_from_map(get_task_environment(service_name, pi, ts, scheduler_config)))
+
+    @staticmethod
+    def _set_readiness_check(t, service_name, pi, ts, override, scheduler_config) -> None:
+        rc = ts.readiness_check
+        if override == GoalStateOverride.PAUSED:
+            rc = ReadinessCheckSpec(PAUSE_READINESS_COMMAND, constants.SHORT_DECLINE_SECONDS,
+                                    constants.SHORT_DECLINE_SECONDS)
+        if rc is None:
+            return
+        c = t.check
+        c.type = P.CheckInfo.COMMAND
+        c.delay_seconds = rc.delay
+        c.interval_seconds = rc.interval
+        c.timeout_seconds = rc.timeout
+        c.command.command.value = rc.command
+        c.command.command.environment.CopyFrom(
+            L.env_from_map(get_task_environment(service_name, pi, ts, scheduler_config)))
+
+    @staticmethod
+    def _executor_info(pi: PodInstance, framework_id: P.FrameworkID, scheduler_config) -> P.ExecutorInfo:
+        e = P.ExecutorInfo(name=pi.pod.type)
+        e.executor_id.value = ""
+        L.set_dcos_space(e, scheduler_config.dcos_space())
+        e.type = P.ExecutorInfo.DEFAULT
+        e.framework_id.CopyFrom(framework_id)
+        e.container.CopyFrom(PodInfoBuilder._container_info(pi.pod, True, False))
+        return e
+
+    @staticmethod
+    def _container_info(pod: PodSpec, add_extra: bool, is_task: bool) -> P.ContainerInfo:
+        c = P.ContainerInfo(type=P.ContainerInfo.MESOS)
+        secret_vols = []
+        for s in pod.secrets:
+            if s.file_path is not None:
+                v = P.Volume(container_path=s.file_path, mode=P.Volume.RO)
+                v.source.type = P.Volume.Source.SECRET
+                v.source.secret.CopyFrom(_reference_secret(s.secret_path))
+                secret_vols.append(v)
+        if is_task:
+            c.linux_info.share_pid_namespace = bool(pod.share_pid_namespace)
+            c.volumes.add(container_path="/tmp", host_path="tmp", mode=P.Volume.RW)
+            if pod.seccomp_unconfined:
+                c.linux_info.seccomp.unconfined = True
+            if pod.seccomp_profile_name:
+                c.linux_info.seccomp.Clear()
+                c.linux_info.seccomp.profile_name = pod.seccomp_profile_name
+        else:
+            if pod.shared_memory is not None:
+                c.linux_info.ipc_mode = P.LinuxInfo.IpcMode.Value(pod.shared_memory.value)
+            if pod.shared_memory_size is not None:
+                c.linux_info.shm_size = pod.shared_memory_size
+        for hv in pod.host_volumes:
+            c.volumes.add(host_path=hv.host_path, container_path=hv.container_path,
+                          mode=P.Volume.Mode.Value(hv.mode) if hv.mode else P.Volume.RW)
+        if not pod.image and not pod.networks and not pod.rlimits and not secret_vols:
+            return c
+        if pod.image and add_extra and is_task:
+            c.mesos.image.type = P.Image.DOCKER
+            c.mesos.image.docker.name = pod.image
+        if pod.networks and not is_task:
+            for n in pod.networks:
+                ni = c.network_infos.add(name=n.name)
+                for hp, cp in n.port_mappings:
+                    ni.port_mappings.add(host_port=hp, container_port=cp)
+                if n.labels:
+                    L.map_to_labels(dict(n.labels), ni.labels)
+        if pod.rlimits and add_extra:
+            for rl in pod.rlimits:
+                r = c.rlimit_info.rlimits.add(type=rl.enum)
+                if rl.soft is not None and rl.hard is not None and rl.soft != RLIMIT_INFINITY and \
+                        rl.hard != RLIMIT_INFINITY:
+                    r.soft = rl.soft
+                    r.hard = rl.hard
+        if add_extra:
+            for v in secret_vols:
+                c.volumes.add().CopyFrom(v)
+        return c
+
+    @staticmethod
+    def _validate(t: P.TaskInfo) -> None:
+        if not t.name:
+            raise InvalidRequirementException(f"TaskInfo must have a name: {t}")
+        if t.task_id.value:
+            try:
+                name = common_id_utils.to_task_name(t.task_id)
+            except L.TaskException as e:
+                raise InvalidRequirementException(f"When non-empty, TaskInfo.id must be a valid ID: {e}")
+            if name != t.name:
+                raise InvalidRequirementException("When non-empty, TaskInfo.id must align with TaskInfo.name")
+        if t.HasField("executor"):
+            raise InvalidRequirementException("TaskInfo must not contain ExecutorInfo.")
+        reader = L.TaskLabelReader(t)
+        try:
+            reader.get_type()
+            reader.get_index()
+        except (L.TaskException, ValueError) as e:
+            raise InvalidRequirementException(str(e))

@@ -1,0 +1,384 @@
+"""Task/reservation label schema and environment helpers.
+
+Reference: sdk/.../offer/taskdata/{LabelConstants,TaskLabelReader,TaskLabelWriter,LabelUtils,
+AttributeStringUtils,AuxLabelAccess,EnvConstants,EnvUtils}.java. Labels written onto every
+``TaskInfo`` (``target_configuration``, ``offer_hostname``, ``task_type``, ``index``, ...) and
+onto every reservation (``resource_id``, ``framework_id``, ``namespace``) are the contract the
+rest of the scheduler -- and the checkpointed state -- relies on.
+"""
+from __future__ import annotations
+
+import base64
+import re
+import uuid
+from typing import Dict, List, Optional
+
+from dcos_commons_amd.mesos import protos as P
+
+BOOLEAN_LABEL_TRUE_VALUE = "true"
+TARGET_CONFIGURATION_LABEL = "target_configuration"
+OFFER_ATTRIBUTES_LABEL = "offer_attributes"
+OFFER_HOSTNAME_LABEL = "offer_hostname"
+OFFER_ZONE_LABEL = "offer_zone"
+OFFER_REGION_LABEL = "offer_region"
+READINESS_CHECK_LABEL = "readiness_check"
+TASK_TYPE_LABEL = "task_type"
+TASK_INDEX_LABEL = "index"
+PERMANENTLY_FAILED_LABEL = "permanently-failed"
+READINESS_CHECK_PASSED_LABEL = "readiness_check_passed"
+RESOURCE_ID_RESERVATION_LABEL = "resource_id"
+FRAMEWORK_ID_RESERVATION_LABEL = "framework_id"
+NAMESPACE_RESERVATION_LABEL = "namespace"
+DCOS_SPACE_EXECUTORINFO_LABEL = "DCOS_SPACE"
+VIP_LABEL_PREFIX = "VIP_"
+VIP_OVERLAY_FLAG_KEY = "network-scope"
+VIP_OVERLAY_FLAG_VALUE = "container"
+VIP_BRIDGE_FLAG_VALUE = "host"
+# MI355X placement: which GPUs of the agent the task was given (comma-separated indices).
+GPU_DEVICES_LABEL = "gpu_devices"
+
+# EnvConstants
+POD_INSTANCE_INDEX_TASKENV = "POD_INSTANCE_INDEX"
+FRAMEWORK_NAME_TASKENV = "FRAMEWORK_NAME"
+TASK_NAME_TASKENV = "TASK_NAME"
+FRAMEWORK_HOST_TASKENV = "FRAMEWORK_HOST"
+FRAMEWORK_VIP_HOST_TASKENV = "FRAMEWORK_VIP_HOST"
+SCHEDULER_API_HOSTNAME_TASKENV = "SCHEDULER_API_HOSTNAME"
+SCHEDULER_API_PORT_TASKENV = "SCHEDULER_API_PORT"
+ZONE_TASKENV = "ZONE"
+REGION_TASKENV = "REGION"
+PLACEMENT_REFERENCED_ZONE_ENV = "PLACEMENT_REFERENCED_ZONE"
+PLACEMENT_REFERENCED_REGION_ENV = "PLACEMENT_REFERENCED_REGION"
+
+
+class TaskException(Exception):
+    pass
+
+
+def labels_to_map(labels: P.Labels) -> Dict[str, str]:
+    return {l.key: l.value for l in labels.labels}
+
+
+def map_to_labels(m: Dict[str, str], out: Optional[P.Labels] = None) -> P.Labels:
+    out = out if out is not None else P.Labels()
+    del out.labels[:]
+    for k in sorted(m):
+        out.labels.add(key=k, value=m[k])
+    return out
+
+
+def encode_health_check(hc: P.HealthCheck) -> str:
+    return base64.b64encode(hc.SerializeToString()).decode("utf-8")
+
+
+def decode_health_check(data: str) -> P.HealthCheck:
+    hc = P.HealthCheck()
+    try:
+        hc.ParseFromString(base64.b64decode(data))
+    except Exception as e:  # noqa: BLE001
+        raise TaskException(str(e))
+    return hc
+
+
+# ---------------------------------------------------------------------------------------
+# attributes
+
+
+def attribute_value_to_string(v: P.Value) -> str:
+    t = v.type
+    if t == P.Value.RANGES:
+        return "[" + ",".join(f"{r.begin}-{r.end}" for r in v.ranges.range) + "]"
+    if t == P.Value.SCALAR:
+        return "%.3f" % v.scalar.value
+    if t == P.Value.SET:
+        return "{" + ",".join(v.set.item) + "}"
+    if t == P.Value.TEXT:
+        return v.text.value
+    raise ValueError(f"Unsupported value type: {v}")
+
+
+def attribute_to_value(attr: P.Attribute) -> P.Value:
+    v = P.Value(type=attr.type)
+    if attr.HasField("ranges"):
+        v.ranges.CopyFrom(attr.ranges)
+    if attr.HasField("scalar"):
+        v.scalar.CopyFrom(attr.scalar)
+    if attr.HasField("set"):
+        v.set.CopyFrom(attr.set)
+    if attr.HasField("text"):
+        v.text.CopyFrom(attr.text)
+    return v
+
+
+def attribute_to_string(attr: P.Attribute) -> str:
+    return f"{attr.name}:{attribute_value_to_string(attribute_to_value(attr))}"
+
+
+def attributes_to_string(attrs) -> str:
+    return ";".join(attribute_to_string(a) for a in attrs)
+
+
+def attribute_string_list(joined: str) -> List[str]:
+    return [t for t in joined.split(";") if t]
+
+
+def attribute_join(name: str, value: str) -> str:
+    return f"{name}:{value}"
+
+
+def attribute_split(attr: str):
+    parts = attr.split(":", 1)
+    if len(parts) != 2:
+        raise ValueError(f"Unable to split attribute into name:value elements: {attr}")
+    return parts[0], parts[1]
+
+
+def text_attribute(name: str, value: str) -> P.Attribute:
+    a = P.Attribute(name=name, type=P.Value.TEXT)
+    a.text.value = value
+    return a
+
+
+def scalar_attribute(name: str, value: float) -> P.Attribute:
+    a = P.Attribute(name=name, type=P.Value.SCALAR)
+    a.scalar.value = value
+    return a
+
+
+# ---------------------------------------------------------------------------------------
+# task labels
+
+
+class TaskLabelReader:
+    def __init__(self, task_info: P.TaskInfo):
+        self._name = task_info.name
+        self._labels = labels_to_map(task_info.labels)
+
+    def _get_or_throw(self, key: str) -> str:
+        v = self._labels.get(key)
+        if v is None:
+            raise TaskException(f"Task {self._name} is missing label {key}. Current labels are: {self._labels}")
+        return v
+
+    def get_type(self) -> str:
+        return self._get_or_throw(TASK_TYPE_LABEL)
+
+    def get_index(self) -> int:
+        return int(self._get_or_throw(TASK_INDEX_LABEL))
+
+    def get_offer_attribute_strings(self) -> List[str]:
+        j = self._labels.get(OFFER_ATTRIBUTES_LABEL)
+        return attribute_string_list(j) if j else []
+
+    def get_zone(self) -> Optional[str]:
+        return self._labels.get(OFFER_ZONE_LABEL)
+
+    def get_region(self) -> Optional[str]:
+        return self._labels.get(OFFER_REGION_LABEL)
+
+    def get_hostname(self) -> str:
+        return self._get_or_throw(OFFER_HOSTNAME_LABEL)
+
+    def get_target_configuration(self) -> uuid.UUID:
+        return uuid.UUID(self._get_or_throw(TARGET_CONFIGURATION_LABEL))
+
+    def get_gpu_devices(self) -> List[int]:
+        v = self._labels.get(GPU_DEVICES_LABEL)
+        return [int(x) for x in v.split(",") if x != ""] if v else []
+
+    def is_readiness_check_succeeded(self, status: P.TaskStatus) -> bool:
+        has_label = READINESS_CHECK_LABEL in self._labels
+        if not has_label and not status.HasField("check_status"):
+            return True
+        if status.HasField("check_status"):
+            cmd = status.check_status.command
+            return cmd.HasField("exit_code") and cmd.exit_code == 0
+        for l in status.labels.labels:
+            if l.key == READINESS_CHECK_PASSED_LABEL:
+                return l.value == BOOLEAN_LABEL_TRUE_VALUE
+        return False
+
+    def is_permanently_failed(self) -> bool:
+        return (self._labels.get(PERMANENTLY_FAILED_LABEL) or "").lower() == "true"
+
+    def has_readiness_check_label(self) -> bool:
+        return READINESS_CHECK_LABEL in self._labels
+
+    def get_readiness_check(self) -> Optional[P.HealthCheck]:
+        v = self._labels.get(READINESS_CHECK_LABEL)
+        return decode_health_check(v) if v else None
+
+
+class TaskLabelWriter:
+    """Mutates the labels of a TaskInfo in place (call :meth:`apply` / ``to_proto``)."""
+
+    def __init__(self, task_info: P.TaskInfo):
+        self._task = task_info
+        self._labels = labels_to_map(task_info.labels)
+
+    def set_additional_labels(self, labels: Dict[str, str]):
+        self._labels.update(labels)
+        return self
+
+    def set_permanently_failed(self):
+        self._labels[PERMANENTLY_FAILED_LABEL] = BOOLEAN_LABEL_TRUE_VALUE
+        return self
+
+    def clear_permanently_failed(self):
+        self._labels.pop(PERMANENTLY_FAILED_LABEL, None)
+        return self
+
+    def set_type(self, t: str):
+        self._labels[TASK_TYPE_LABEL] = t
+        return self
+
+    def set_index(self, i: int):
+        self._labels[TASK_INDEX_LABEL] = str(i)
+        return self
+
+    def set_offer_attributes(self, offer: P.Offer):
+        self._labels[OFFER_ATTRIBUTES_LABEL] = attributes_to_string(offer.attributes)
+        return self
+
+    def set_zone(self, zone: str):
+        self._labels[OFFER_ZONE_LABEL] = zone
+        return self
+
+    def set_region(self, region: str):
+        self._labels[OFFER_REGION_LABEL] = region
+        return self
+
+    def set_hostname(self, offer: P.Offer):
+        self._labels[OFFER_HOSTNAME_LABEL] = offer.hostname
+        return self
+
+    def set_target_configuration(self, config_id):
+        self._labels[TARGET_CONFIGURATION_LABEL] = str(config_id)
+        return self
+
+    def set_gpu_devices(self, devices: List[int]):
+        self._labels[GPU_DEVICES_LABEL] = ",".join(str(d) for d in devices)
+        return self
+
+    def set_readiness_check(self, hc: P.HealthCheck):
+        c = P.HealthCheck()
+        c.CopyFrom(hc)
+        c.consecutive_failures = 0
+        self._labels[READINESS_CHECK_LABEL] = encode_health_check(c)
+        return self
+
+    def get_readiness_check(self) -> Optional[P.HealthCheck]:
+        v = self._labels.get(READINESS_CHECK_LABEL)
+        return decode_health_check(v) if v else None
+
+    def set_readiness_check_envvar(self, key: str, value: str):
+        hc = self.get_readiness_check()
+        if hc is None:
+            return self
+        env = with_env_var(hc.command.environment, key, value)
+        hc.command.environment.CopyFrom(env)
+        return self.set_readiness_check(hc)
+
+    def to_proto(self) -> P.Labels:
+        return map_to_labels(self._labels)
+
+    def apply(self) -> P.TaskInfo:
+        map_to_labels(self._labels, self._task.labels)
+        return self._task
+
+
+# ---------------------------------------------------------------------------------------
+# reservation labels (AuxLabelAccess)
+
+
+def _reservation_label(reservation: P.Resource.ReservationInfo, key: str) -> Optional[str]:
+    for l in reservation.labels.labels:
+        if l.key == key:
+            return l.value
+    return None
+
+
+def get_resource_id(reservation) -> Optional[str]:
+    return _reservation_label(reservation, RESOURCE_ID_RESERVATION_LABEL)
+
+
+def get_framework_id(reservation) -> Optional[str]:
+    return _reservation_label(reservation, FRAMEWORK_ID_RESERVATION_LABEL)
+
+
+def get_resource_namespace(reservation) -> Optional[str]:
+    return _reservation_label(reservation, NAMESPACE_RESERVATION_LABEL)
+
+
+def set_reservation_label(reservation, key: str, value: str) -> None:
+    m = labels_to_map(reservation.labels)
+    m[key] = value
+    map_to_labels(m, reservation.labels)
+
+
+def set_dcos_space(executor_info: P.ExecutorInfo, space: str) -> None:
+    m = labels_to_map(executor_info.labels)
+    m[DCOS_SPACE_EXECUTORINFO_LABEL] = space
+    map_to_labels(m, executor_info.labels)
+
+
+def set_vip_labels(port: P.Port, vip_name: str, vip_port: int, network_names, supports_port_mapping) -> None:
+    m = labels_to_map(port.labels)
+    m[f"{VIP_LABEL_PREFIX}{uuid.uuid4()}"] = f"{vip_name}:{vip_port}"
+    if network_names:
+        use_host_ip = any(supports_port_mapping(n) for n in network_names)
+        m[VIP_OVERLAY_FLAG_KEY] = VIP_BRIDGE_FLAG_VALUE if use_host_ip else VIP_OVERLAY_FLAG_VALUE
+    map_to_labels(m, port.labels)
+
+
+def get_vips_from_labels(port: P.Port):
+    out = []
+    for l in port.labels.labels:
+        if not l.key.startswith(VIP_LABEL_PREFIX):
+            continue
+        parts = l.value.split(":")
+        if len(parts) != 2:
+            continue
+        try:
+            out.append((parts[0], int(parts[1])))
+        except ValueError:
+            continue
+    return out
+
+
+# ---------------------------------------------------------------------------------------
+# environment (EnvUtils)
+
+_ENV_INVALID = re.compile(r"[^a-zA-Z0-9_]")
+
+
+def to_env_name(s: str) -> str:
+    return _ENV_INVALID.sub("_", s.upper())
+
+
+def env_to_map(env: P.Environment) -> Dict[str, str]:
+    return {v.name: v.value for v in env.variables}
+
+
+def env_from_map(m: Dict[str, str]) -> P.Environment:
+    env = P.Environment()
+    for k in sorted(m):
+        env.variables.add(name=k, value=m[k])
+    return env
+
+
+def with_env_var(env: P.Environment, key: str, value: str) -> P.Environment:
+    vars_ = {v.name: v for v in env.variables}
+    nv = P.Environment.Variable(name=key, value=value)
+    vars_[key] = nv
+    out = P.Environment()
+    for k in sorted(vars_):
+        out.variables.add().CopyFrom(vars_[k])
+    return out
+
+
+def get_env_var(env: P.Environment, key: str) -> Optional[str]:
+    for v in env.variables:
+        if v.name == key:
+            return v.value
+    return None

@@ -1,0 +1,123 @@
+"""Common service-scheduler logic.
+
+Reference: sdk/.../scheduler/AbstractScheduler.java:36-262. ``get_client_status`` snapshots the
+candidate steps and updates the WorkSetTracker; ``offers`` refuses to launch until explicit
+reconciliation has finished; ``task_status`` stores the status and feeds the reconciler.
+"""
+from __future__ import annotations
+
+import logging
+from typing import List, Optional
+
+from dcos_commons_amd.framework.process_exit import ProcessExit
+from dcos_commons_amd.scheduler.mesos_event_client import (
+    MesosEventClient,
+    OfferResponse,
+    TaskStatusResponse,
+)
+from dcos_commons_amd.scheduler.reconciliation import ExplicitReconciler, WorkSetTracker
+from dcos_commons_amd.state.state_store import StateStoreException
+from dcos_commons_amd.storage.persister import Reason
+
+
+class AbstractScheduler(MesosEventClient):
+    def __init__(self, service_spec, scheduler_config, state_store, plan_coordinator, plan_customizer=None,
+                 namespace: Optional[str] = None):
+        self.service_spec = service_spec
+        self.scheduler_config = scheduler_config
+        self.state_store = state_store
+        self.plan_coordinator = plan_coordinator
+        self.plan_customizer = plan_customizer
+        self.namespace = namespace
+        self.candidate_steps: List = []
+        self.work_set_tracker: Optional[WorkSetTracker] = None
+        self.reconciler: Optional[ExplicitReconciler] = None
+        self.logger = logging.getLogger(type(self).__module__ + (f"({namespace})" if namespace else ""))
+
+    def customize_plans(self) -> None:
+        if self.plan_customizer is None:
+            return
+        for pm in self.plan_coordinator.get_plan_managers():
+            plan = pm.get_plan()
+            if plan.is_recovery_plan():
+                continue
+            pm.set_plan(self.plan_customizer.update_plan(plan))
+
+    def get_plans(self):
+        return [pm.get_plan() for pm in self.plan_coordinator.get_plan_managers()]
+
+    def get_plan(self, name: str):
+        for p in self.get_plans():
+            if p.get_name() == name:
+                return p
+        return None
+
+    def registered(self, re_registered: bool) -> None:
+        if not re_registered or self.reconciler is None:
+            self.work_set_tracker = WorkSetTracker(self.namespace)
+            self.reconciler = ExplicitReconciler(self.state_store, self.namespace)
+            self.registered_with_mesos()
+        self.reconciler.start()
+        self.reconciler.reconcile()
+
+    def _in_progress_steps(self):
+        out = []
+        for pm in self.plan_coordinator.get_plan_managers():
+            for phase in pm.get_plan().get_children():
+                for step in phase.get_children():
+                    if step.is_running():
+                        out.append(step)
+        return out
+
+    def get_client_status(self):
+        self.candidate_steps = list(self.plan_coordinator.get_candidates())
+        active = list(self.candidate_steps)
+        seen = {id(s) for s in active}
+        for s in self._in_progress_steps():
+            if id(s) not in seen:
+                active.append(s)
+        if self.work_set_tracker is None:
+            self.logger.error("WorkSetTracker is uninitialized (status requested before registration)")
+            ProcessExit.exit(ProcessExit.ERROR, RuntimeError("WorkSetTracker uninitialized"))
+        self.work_set_tracker.update_work_set(active)
+        return self.get_status()
+
+    def offers(self, offers) -> OfferResponse:
+        self.reconciler.reconcile()
+        if not self.reconciler.is_reconciled():
+            self.logger.info("Not ready for offers: waiting for task reconciliation to complete.")
+            return OfferResponse.not_ready([])
+        return self.process_offers(offers, self.candidate_steps)
+
+    def task_status(self, status) -> TaskStatusResponse:
+        try:
+            self.process_status_update(status)
+            if self.reconciler is not None:
+                self.reconciler.update(status)
+        except StateStoreException as e:
+            if e.reason == Reason.NOT_FOUND:
+                self.logger.info("Status for unknown task %s: %s", status.task_id.value, e)
+                return TaskStatusResponse.unknown_task()
+            self.logger.warning("Failed to update TaskStatus received from Mesos: %s", e)
+        except Exception as e:  # noqa: BLE001
+            self.logger.warning("Failed to update TaskStatus received from Mesos: %s", e)
+        return TaskStatusResponse.processed()
+
+    # abstract
+    def registered_with_mesos(self) -> None:
+        raise NotImplementedError
+
+    def get_status(self):
+        raise NotImplementedError
+
+    def process_offers(self, offers, steps) -> OfferResponse:
+        raise NotImplementedError
+
+    def process_status_update(self, status) -> None:
+        raise NotImplementedError
+
+    def get_config_store(self):
+        raise NotImplementedError
+
+    def get_custom_endpoints(self):
+        return {}

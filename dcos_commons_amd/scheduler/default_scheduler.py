@@ -1,0 +1,220 @@
+"""The standard service scheduler.
+
+Reference: sdk/.../scheduler/DefaultScheduler.java:81-585. Wires the plan scheduler, offer
+evaluator, launch recorder, decommission recorder, debug trackers and HTTP resources; implements
+the status logic (deploy-completion bit, FINISH goal -> uninstall, footprint vs launch), the
+unexpected-reservation garbage collector and status-update processing.
+"""
+from __future__ import annotations
+
+import logging
+from typing import Dict, List, Optional
+
+from dcos_commons_amd.framework import task_killer
+from dcos_commons_amd.http import endpoint_utils
+from dcos_commons_amd.mesos import protos as P
+from dcos_commons_amd.offer.evaluate.offer_evaluator import OfferEvaluator
+from dcos_commons_amd.offer.history import OfferOutcomeTracker, OfferOutcomeTrackerV2
+from dcos_commons_amd.offer.resources import get_all_resources, get_resource_id, get_resource_ids
+from dcos_commons_amd.scheduler.abstract_scheduler import AbstractScheduler
+from dcos_commons_amd.scheduler.decommission import DECOMMISSIONING_STATUS
+from dcos_commons_amd.scheduler.mesos_event_client import (
+    ClientStatusResponse,
+    OfferResources,
+    OfferResponse,
+    UnexpectedResourcesResponse,
+)
+from dcos_commons_amd.scheduler.plan.elements import get_launchable_tasks
+from dcos_commons_amd.scheduler.plan.managers import DecommissionPlanManager
+from dcos_commons_amd.scheduler.plan.plan_scheduler import PlanScheduler
+from dcos_commons_amd.scheduler.plan.pod_instance_requirement import RecoveryType
+from dcos_commons_amd.scheduler.plan.status import Status
+from dcos_commons_amd.scheduler.recovery import RecoveryStep, is_permanently_failed
+from dcos_commons_amd.scheduler.uninstall import UninstallRecorder
+from dcos_commons_amd.specification.specs import GoalState
+from dcos_commons_amd.state import state_store_utils
+from dcos_commons_amd.state.persistent_launch_recorder import PersistentLaunchRecorder
+
+
+def _is_working(plan) -> bool:
+    st = plan.get_status()
+    if st in (Status.PENDING, Status.IN_PROGRESS, Status.PREPARED, Status.STARTED, Status.STARTING):
+        return True
+    if st in (Status.DELAYED, Status.COMPLETE, Status.ERROR, Status.WAITING):
+        return False
+    raise ValueError(f"Unsupported status in {plan.get_name()} plan: {st}")
+
+
+def _is_replacing(recovery_pm) -> bool:
+    plan = recovery_pm.get_plan()
+    if plan.is_complete():
+        return False
+    for phase in plan.get_children():
+        if phase.is_complete():
+            continue
+        for step in phase.get_children():
+            if not step.is_complete() and isinstance(step, RecoveryStep) and \
+                    step.recovery_type == RecoveryType.PERMANENT:
+                return True
+    return False
+
+
+class DefaultScheduler(AbstractScheduler):
+    def __init__(self, service_spec, scheduler_config, namespace: Optional[str], custom_resources, plan_coordinator,
+                 plan_customizer, framework_store, state_store, config_store, template_url_factory=None,
+                 custom_endpoint_producers: Optional[Dict] = None, tls_stage_factory=None):
+        super().__init__(service_spec, scheduler_config, state_store, plan_coordinator, plan_customizer, namespace)
+        self.framework_store = framework_store
+        self.config_store = config_store
+        self.goal_state = service_spec.goal
+        self.custom_resources = list(custom_resources or [])
+        self.custom_endpoint_producers = dict(custom_endpoint_producers or {})
+        self.launch_recorder = PersistentLaunchRecorder(state_store, service_spec, namespace)
+        decom = self._decommission_manager()
+        self.decommission_recorder = (UninstallRecorder(state_store, decom.resource_steps)
+                                      if decom is not None else None)
+        pms = plan_coordinator.get_plan_managers()
+        self.deployment_plan_manager = next(pm for pm in pms if pm.get_plan().is_deploy_plan())
+        self.recovery_plan_manager = next(pm for pm in pms if pm.get_plan().is_recovery_plan())
+        self._deployment_completion_stored = False
+        self.offer_outcome_tracker = None if namespace else OfferOutcomeTracker()
+        self.offer_outcome_tracker_v2 = None if namespace else OfferOutcomeTrackerV2()
+        if template_url_factory is None:
+            template_url_factory = endpoint_utils.template_url_factory(service_spec.name, scheduler_config)
+        self.offer_evaluator = OfferEvaluator(
+            framework_store, state_store, service_spec.name, config_store.get_target_config(),
+            template_url_factory, scheduler_config, namespace, self.offer_outcome_tracker,
+            self.offer_outcome_tracker_v2, tls_stage_factory)
+        self.plan_scheduler = PlanScheduler(self.offer_evaluator, state_store, namespace)
+        self.customize_plans()
+
+    def _decommission_manager(self) -> Optional[DecommissionPlanManager]:
+        for pm in self.plan_coordinator.get_plan_managers():
+            if pm.get_plan().is_decommission_plan():
+                return pm
+        return None
+
+    def get_config_store(self):
+        return self.config_store
+
+    def get_custom_endpoints(self):
+        return self.custom_endpoint_producers
+
+    def get_http_endpoints(self):
+        from dcos_commons_amd.http import resources as R
+
+        out = list(self.custom_resources)
+        out.append(R.ArtifactResource(self.config_store))
+        out.append(R.ConfigResource(self.config_store))
+        out.append(R.EndpointsResource(self.state_store, self.service_spec.name, self.scheduler_config,
+                                       self.custom_endpoint_producers))
+        out.append(R.PlansResource(self.plan_coordinator.get_plan_managers()))
+        out.append(R.HealthResource(self.plan_coordinator, self.framework_store))
+        out.append(R.PodResource(self.state_store, self.config_store, self.service_spec.name))
+        out.append(R.StateResource(self.framework_store, self.state_store))
+        out.append(R.DebugResource(self))
+        return out
+
+    def registered_with_mesos(self) -> None:
+        active = get_launchable_tasks(self.get_plans())
+        decom = self._decommission_manager()
+        if decom is not None:
+            active |= {t.name for t in decom.tasks_to_decommission}
+        unneeded = [t for t in self.state_store.fetch_tasks() if t.name not in active]
+        if self.scheduler_config.use_legacy_unneeded_task_kills():
+            for t in unneeded:
+                c = P.TaskInfo()
+                c.CopyFrom(t)
+                c.task_id.value = ""
+                self.state_store.clear_task(t.name)
+                self.state_store.store_tasks([c])
+            for t in unneeded:
+                task_killer.kill_task(t.task_id)
+            from dcos_commons_amd.state.goal_state_override import OverrideProgress
+
+            for t in self.state_store.fetch_tasks():
+                if self.state_store.fetch_goal_override_status(t.name).progress == OverrideProgress.PENDING:
+                    task_killer.kill_task(t.task_id)
+        else:
+            for t in unneeded:
+                task_killer.kill_task(t.task_id)
+
+    def unregistered(self) -> None:
+        raise NotImplementedError("Should not have received unregistered call. "
+                                  "This is only applicable to UninstallSchedulers")
+
+    def get_status(self) -> ClientStatusResponse:
+        pms = self.plan_coordinator.get_plan_managers()
+        all_delayed_or_complete = all(pm.get_plan().is_complete() or pm.get_plan().is_delayed() for pm in pms)
+        deploy_completed = self.deployment_plan_manager.get_plan().is_complete()
+        if deploy_completed and not self._deployment_completion_stored:
+            state_store_utils.set_deployment_was_completed(self.state_store)
+            self._deployment_completion_stored = True
+        if (self.goal_state == GoalState.FINISH and deploy_completed
+                and self.recovery_plan_manager.get_plan().is_complete()):
+            return ClientStatusResponse.ready_to_uninstall()
+        if all_delayed_or_complete:
+            return ClientStatusResponse.idle()
+        if not deploy_completed or _is_replacing(self.recovery_plan_manager):
+            return ClientStatusResponse.footprint(self.work_set_tracker.has_new_work())
+        if any(_is_working(pm.get_plan()) for pm in pms):
+            return ClientStatusResponse.launching(self.work_set_tracker.has_new_work())
+        return ClientStatusResponse.idle()
+
+    def process_offers(self, offers, steps) -> OfferResponse:
+        recs = self.plan_scheduler.resource_offers(offers, steps)
+        try:
+            self.launch_recorder.record(recs)
+            if self.decommission_recorder is not None:
+                self.decommission_recorder.record_decommission(recs)
+        except Exception:  # noqa: BLE001
+            self.logger.exception("Failed to record offer operations, returning empty operations list")
+            recs = []
+        return OfferResponse.processed(recs)
+
+    def get_unexpected_resources(self, unused_offers) -> UnexpectedResourcesResponse:
+        try:
+            keep = set()
+            for t in self.state_store.fetch_tasks():
+                if is_permanently_failed(t):
+                    continue
+                if self.state_store.fetch_goal_override_status(t.name) == DECOMMISSIONING_STATUS:
+                    continue
+                keep.update(get_resource_ids(get_all_resources(t)))
+        except Exception:  # noqa: BLE001
+            self.logger.exception("Failed to fetch expected tasks to determine unexpected resources")
+            return UnexpectedResourcesResponse.failed([])
+        unexpected = []
+        for offer in unused_offers:
+            o = OfferResources(offer)
+            for r in offer.resources:
+                rid = get_resource_id(r)
+                if rid is not None and rid not in keep:
+                    o.add(r)
+            if o.resources:
+                unexpected.append(o)
+        if self.decommission_recorder is not None:
+            try:
+                self.decommission_recorder.record_cleanup_or_uninstall(unexpected)
+            except Exception:  # noqa: BLE001
+                self.logger.exception("Failed to record unexpected resources in decommission recorder")
+                return UnexpectedResourcesResponse.failed([])
+        return UnexpectedResourcesResponse.processed(unexpected)
+
+    def process_status_update(self, status: P.TaskStatus) -> None:
+        name = state_store_utils.fetch_task_info(self.state_store, status).name
+        self.state_store.store_status(name, status)
+        for pm in self.plan_coordinator.get_plan_managers():
+            pm.update(status)
+        if status.HasField("container_status") and any(
+                len(ni.ip_addresses) > 0 for ni in status.container_status.network_infos):
+            try:
+                state_store_utils.store_task_status_as_property(self.state_store, name, status)
+            except Exception as e:  # noqa: BLE001
+                self.logger.warning("Unable to store network info for status update: %s", e)
+
+    def to_uninstall_scheduler(self):
+        from dcos_commons_amd.scheduler.uninstall import UninstallScheduler
+
+        return UninstallScheduler(self.service_spec, self.state_store, self.config_store, self.scheduler_config,
+                                  self.plan_customizer, self.namespace, self.framework_store)

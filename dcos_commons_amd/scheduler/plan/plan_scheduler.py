@@ -1,0 +1,73 @@
+"""Matches candidate steps against offers.
+
+Reference: sdk/.../scheduler/plan/PlanScheduler.java:27-166. For each candidate step, in order:
+``step.start()``, kill the live tasks sharing the resource sets about to be relaunched, run the
+``OfferEvaluator``, hand the recommendations to the step, and remove consumed offers before the
+next step (greedy).
+"""
+from __future__ import annotations
+
+import logging
+from typing import List, Optional
+
+from dcos_commons_amd.framework import task_killer
+from dcos_commons_amd.offer.task_utils import is_terminal
+
+LOGGER = logging.getLogger(__name__)
+
+
+class PlanScheduler:
+    def __init__(self, offer_evaluator, state_store, namespace: Optional[str] = None):
+        self.offer_evaluator = offer_evaluator
+        self.state_store = state_store
+        self.logger = logging.getLogger(__name__ + (f"({namespace})" if namespace else ""))
+
+    def resource_offers(self, offers, steps) -> list:
+        all_recs = []
+        available = list(offers)
+        # Launches are only recorded after the whole cycle (write-ahead, then ACCEPT), so the
+        # stored task set is constant across the steps of one cycle: read it once.
+        all_tasks = {t.name: t for t in self.state_store.fetch_tasks()} if steps else {}
+        for step in steps:
+            recs = self._step_offers(available, step, all_tasks)
+            if recs:
+                all_recs.extend(recs)
+                used = {r.offer_id.value for r in recs}
+                available = [o for o in available if o.id.value not in used]
+        return all_recs
+
+    def _step_offers(self, offers, step, all_tasks) -> list:
+        if not (step.is_pending() or step.is_prepared()):
+            return []
+        step.start()
+        req = step.get_pod_instance_requirement()
+        if req is None:
+            step.update_offer_status([])
+            return []
+        self._kill_tasks(req)
+        try:
+            recs = self.offer_evaluator.evaluate(req, offers, all_tasks)
+        except Exception:  # noqa: BLE001
+            self.logger.exception("Failed generate OfferRecommendations.")
+            return []
+        if not recs:
+            self.logger.info("Unable to find any offers which fulfill requirement provided by step %s",
+                             step.get_name())
+            step.update_offer_status([])
+            return []
+        step.update_offer_status([r for r in recs if r.get_operation() is not None])
+        return recs
+
+    def _kill_tasks(self, req) -> None:
+        pi = req.pod_instance
+        sets = {t.resource_set.id for t in pi.pod.tasks if t.name in req.tasks_to_launch}
+        for t in pi.pod.tasks:
+            if t.resource_set.id not in sets:
+                continue
+            name = f"{pi.name}-{t.name}"
+            info = self.state_store.fetch_task(name)
+            if info is None:
+                continue
+            status = self.state_store.fetch_status(name)
+            if status is None or not is_terminal(status):
+                task_killer.kill_task(info.task_id)

@@ -1,0 +1,205 @@
+"""Scheduler flag system: ~45 environment variables with defaults.
+
+Reference: sdk/.../scheduler/SchedulerConfig.java:56-666. The defaults here are identical to the
+reference; MI355X-specific additions are prefixed ``SDK_`` and documented inline.
+"""
+from __future__ import annotations
+
+from typing import Dict, Optional
+
+from dcos_commons_amd.framework.env_store import EnvStore
+from dcos_commons_amd.mesos import protos as P
+from dcos_commons_amd.state.goal_state_override import PAUSE_COMMAND
+
+DEFAULT_SCHEDULER_ROLE = "slave_public"
+MESOS_API_VERSION_V1 = "V1"
+
+
+def _scalar(v: float) -> P.Value:
+    val = P.Value(type=P.Value.SCALAR)
+    val.scalar.value = v
+    return val
+
+
+class SchedulerConfig:
+    def __init__(self, env_store: Optional[EnvStore] = None):
+        self.env = env_store or EnvStore.from_env()
+
+    @staticmethod
+    def from_env() -> "SchedulerConfig":
+        return SchedulerConfig(EnvStore.from_env())
+
+    @staticmethod
+    def from_map(m: Dict[str, str]) -> "SchedulerConfig":
+        return SchedulerConfig(EnvStore.from_map(m))
+
+    @staticmethod
+    def for_testing(**overrides) -> "SchedulerConfig":
+        """Equivalent of the reference's SchedulerConfigTestUtils.getTestSchedulerConfig()."""
+        env = {
+            "PORT_API": "8080",
+            "BOOTSTRAP_URI": "bootstrap-uri",
+            "LIBMESOS_URI": "libmesos-uri",
+            "JAVA_URI": "java-uri",
+            "JAVA_HOME": "java-home",
+            "PACKAGE_NAME": "test-package",
+            "PACKAGE_VERSION": "1.0",
+            "PACKAGE_BUILD_TIME_EPOCH_MS": "0",
+            "LIBPROCESS_IP": "127.0.0.1",
+            "DISABLE_DEADLOCK_EXIT": "true",
+        }
+        env.update({k: str(v) for k, v in overrides.items()})
+        return SchedulerConfig(EnvStore.from_map(env))
+
+    # timeouts
+    def api_server_init_timeout_s(self) -> int:
+        return self.env.get_optional_int("API_SERVER_TIMEOUT_S", 600)
+
+    def multi_service_removal_timeout_s(self) -> int:
+        return self.env.get_optional_int("SERVICE_REMOVAL_TIMEOUT_S", 600)
+
+    def multi_service_reserve_discipline(self) -> int:
+        return self.env.get_optional_int("RESERVE_DISCIPLINE", 0)
+
+    def auth_token_refresh_threshold_s(self) -> int:
+        return self.env.get_optional_int("AUTH_TOKEN_REFRESH_THRESHOLD_S", 30)
+
+    # executor
+    def executor_resources(self) -> Dict[str, P.Value]:
+        return {
+            "cpus": _scalar(self.env.get_optional_double("EXECUTOR_CPUS", 0.1)),
+            "disk": _scalar(self.env.get_optional_double("EXECUTOR_DISK_MB", 256)),
+            "mem": _scalar(self.env.get_optional_double("EXECUTOR_MEM_MB", 32)),
+        }
+
+    # identity / uris
+    def api_server_port(self) -> int:
+        return self.env.get_required_int("PORT_API")
+
+    def bootstrap_uri(self) -> str:
+        return self.env.get_optional("BOOTSTRAP_URI", "")
+
+    def libmesos_uri(self) -> str:
+        return self.env.get_optional("LIBMESOS_URI", "")
+
+    def java_uri(self) -> str:
+        return self.env.get_optional("JAVA_URI", "")
+
+    def java_home(self) -> str:
+        return self.env.get_optional("JAVA_HOME", "")
+
+    def dcos_space(self) -> str:
+        v = self.env.get_optional("DCOS_SPACE", None)
+        if v is not None:
+            return v
+        return self.env.get_optional("MARATHON_APP_ID", "/")
+
+    def scheduler_region(self) -> Optional[str]:
+        return self.env.get_optional("SERVICE_REGION", None)
+
+    def service_namespace(self) -> Optional[str]:
+        if self.env.get_optional_boolean("MARATHON_APP_ENFORCE_GROUP_ROLE", False):
+            return self.env.get_required("MESOS_ALLOCATION_ROLE")
+        preferred = self.env.get_optional("MESOS_ALLOCATION_ROLE", None)
+        if preferred is not None and preferred != DEFAULT_SCHEDULER_ROLE:
+            return preferred
+        return None
+
+    def enable_role_migration(self) -> bool:
+        return self.env.get_optional_boolean("ENABLE_ROLE_MIGRATION", False)
+
+    def secrets_namespace(self, service_name: str) -> str:
+        ns = self.dcos_space().lstrip("/")
+        return ns if ns else service_name
+
+    # switches
+    def is_state_cache_enabled(self) -> bool:
+        return not self.env.is_present("DISABLE_STATE_CACHE")
+
+    def is_deadlock_exit_enabled(self) -> bool:
+        return not self.env.is_present("DISABLE_DEADLOCK_EXIT")
+
+    def is_suppress_enabled(self) -> bool:
+        return not self.env.is_present("DISABLE_SUPPRESS")
+
+    def is_uninstall_enabled(self) -> bool:
+        return self.env.is_present("SDK_UNINSTALL")
+
+    def use_legacy_unneeded_task_kills(self) -> bool:
+        return self.env.is_present("USE_LEGACY_KILL_UNNEEDED_TASKS")
+
+    def is_side_channel_active(self) -> bool:
+        return self.env.is_present("DCOS_SERVICE_ACCOUNT_CREDENTIAL")
+
+    def side_channel_credential(self) -> Optional[str]:
+        return self.env.get_optional("DCOS_SERVICE_ACCOUNT_CREDENTIAL", None)
+
+    # statsd
+    def statsd_poll_interval_s(self) -> int:
+        return self.env.get_optional_long("STATSD_POLL_INTERVAL_S", 10)
+
+    def statsd_host(self) -> Optional[str]:
+        return self.env.get_optional("STATSD_UDP_HOST", None)
+
+    def statsd_port(self) -> Optional[int]:
+        v = self.env.get_optional("STATSD_UDP_PORT", None)
+        return int(v) if v else None
+
+    # mesos
+    def mesos_api_version(self) -> str:
+        return self.env.get_optional("MESOS_API_VERSION", MESOS_API_VERSION_V1)
+
+    def mesos_master_url(self) -> str:
+        """MI355X build: the v1 HTTP endpoint of the master (``SDK_MESOS_MASTER``)."""
+        return self.env.get_optional("SDK_MESOS_MASTER", "http://leader.mesos:5050")
+
+    def pause_override_cmd(self) -> str:
+        return self.env.get_optional("PAUSE_OVERRIDE_CMD", PAUSE_COMMAND)
+
+    def autoip_tld(self) -> str:
+        return self.env.get_optional("SERVICE_TLD", "autoip.dcos.thisdcos.directory")
+
+    def vip_tld(self) -> str:
+        return self.env.get_optional("VIP_TLD", "l4lb.thisdcos.directory")
+
+    def marathon_name(self) -> str:
+        return self.env.get_optional("MARATHON_NAME", "marathon")
+
+    def implicit_reconcile_delay_ms(self) -> int:
+        return self.env.get_optional_long("IMPLICIT_RECONCILIATION_DELAY_MS", 0)
+
+    def implicit_reconcile_period_ms(self) -> int:
+        return self.env.get_optional_long("IMPLICIT_RECONCILIATION_PERIOD_MS", 60 * 60 * 1000)
+
+    def is_region_awareness_enabled(self) -> bool:
+        return self.env.get_optional_boolean("ALLOW_REGION_AWARENESS", True)
+
+    def scheduler_ip(self) -> str:
+        return self.env.get_optional("LIBPROCESS_IP", "127.0.0.1")
+
+    # backoff (reference plan/backoff/Backoff.java:17-50)
+    def is_backoff_enabled(self) -> bool:
+        return self.env.get_optional_boolean("ENABLE_BACKOFF", False)
+
+    def backoff_factor(self) -> float:
+        return self.env.get_optional_double("FRAMEWORK_BACKOFF_FACTOR", 1.15)
+
+    def initial_backoff_s(self) -> int:
+        return self.env.get_optional_int("FRAMEWORK_INITIAL_BACKOFF", 60)
+
+    def max_launch_delay_s(self) -> int:
+        return self.env.get_optional_int("FRAMEWORK_MAX_LAUNCH_DELAY", 300)
+
+    # offer processing cadence (reference OfferProcessor.java:46 hard-codes 5 s; the
+    # event-driven MI355X build wakes immediately on offers/status updates and uses this only
+    # as the idle poll interval).
+    def offer_wait_s(self) -> float:
+        return self.env.get_optional_double("SDK_OFFER_WAIT_S", 5.0)
+
+    def build_info(self) -> Dict[str, str]:
+        return {
+            "PACKAGE_NAME": self.env.get_optional("PACKAGE_NAME", ""),
+            "PACKAGE_VERSION": self.env.get_optional("PACKAGE_VERSION", ""),
+            "SDK_NAME": "dcos-commons-amd",
+            "SDK_VERSION": "0.58.0-mi355x",
+        }

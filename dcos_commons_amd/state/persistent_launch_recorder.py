@@ -1,0 +1,73 @@
+"""Write-ahead recording of launches.
+
+Reference: sdk/.../state/PersistentLaunchRecorder.java:32-212. Every ``StoreTaskInfoRecommendation``
+is persisted *before* the ACCEPT is sent (empty-TaskID entries first), together with a synthetic
+``TASK_STAGING`` status for real launches; tasks sharing a resource set with the launched task get
+the new resources copied onto their stored TaskInfo.
+"""
+from __future__ import annotations
+
+import logging
+from typing import Optional
+
+from dcos_commons_amd.mesos import protos as P
+from dcos_commons_amd.offer import task_utils
+from dcos_commons_amd.offer.recommendations import StoreTaskInfoRecommendation
+from dcos_commons_amd.offer.taskdata.labels import TaskException, TaskLabelReader
+from dcos_commons_amd.specification.specs import PodInstance
+
+
+class PersistentLaunchRecorder:
+    def __init__(self, state_store, service_spec, namespace: Optional[str] = None):
+        self.state_store = state_store
+        self.service_spec = service_spec
+        self.logger = logging.getLogger(__name__ + (f"({namespace})" if namespace else ""))
+
+    def record(self, recommendations) -> None:
+        stores = [r for r in recommendations if isinstance(r, StoreTaskInfoRecommendation)]
+        stores.sort(key=lambda r: len(r.task_info.task_id.value))
+        for rec in stores:
+            info = rec.state_store_task_info()
+            status = None
+            if info.task_id.value != "":
+                status = P.TaskStatus(state=P.TASK_STAGING)
+                status.task_id.CopyFrom(info.task_id)
+                if info.HasField("executor"):
+                    status.executor_id.CopyFrom(info.executor.executor_id)
+            pi = self._pod_instance(info)
+            if pi is not None:
+                self._update_resource_set_peers(pi, info)
+            self.state_store.store_tasks([info])
+            if status is not None:
+                self.state_store.store_status(info.name, status)
+
+    def _pod_instance(self, info: P.TaskInfo) -> Optional[PodInstance]:
+        try:
+            pod = task_utils.get_pod_spec(self.service_spec, info)
+            return PodInstance(pod, TaskLabelReader(info).get_index()) if pod is not None else None
+        except (TaskException, ValueError):
+            return None
+
+    def _update_resource_set_peers(self, pi: PodInstance, info: P.TaskInfo) -> None:
+        spec = task_utils.get_task_spec(pi, info.name)
+        if spec is None:
+            return
+        peers = []
+        for t in pi.pod.tasks:
+            if t.name == spec.name or t.resource_set != spec.resource_set:
+                continue
+            peer = self.state_store.fetch_task(f"{pi.name}-{t.name}")
+            if peer is not None:
+                peers.append(peer)
+        updated = []
+        for peer in peers:
+            c = P.TaskInfo()
+            c.CopyFrom(peer)
+            del c.resources[:]
+            c.resources.extend(info.resources)
+            if info.HasField("executor"):
+                del c.executor.resources[:]
+                c.executor.resources.extend(info.executor.resources)
+            updated.append(c)
+        if updated:
+            self.state_store.store_tasks(updated)

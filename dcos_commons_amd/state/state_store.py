@@ -1,0 +1,289 @@
+"""Persistent task state: TaskInfo / TaskStatus / goal overrides / properties.
+
+Reference: sdk/.../state/StateStore.java:58-688. Layout (per service namespace)::
+
+    Tasks/<pod>-<i>-<task>/TaskInfo                    protobuf TaskInfo bytes
+    Tasks/<pod>-<i>-<task>/TaskStatus                  protobuf TaskStatus bytes
+    Tasks/<pod>-<i>-<task>/Metadata/goal-state-override
+    Tasks/<pod>-<i>-<task>/Metadata/override-status
+    Properties/<key>                                   raw bytes (<= 1 MB)
+
+TaskInfo writes are batched into <= 1 MB ``set_many`` transactions (StateStore.java:213).
+A status that would move an already-terminal task to LOST/GONE/... is rejected, as is a
+status whose TaskID differs from the stored one (other than the synthetic STAGING).
+"""
+from __future__ import annotations
+
+import logging
+from typing import Collection, Dict, List, Optional
+
+from dcos_commons_amd.mesos import protos as P
+from dcos_commons_amd.storage.persister import Persister, PersisterException, Reason
+from dcos_commons_amd.storage.persister_utils import (
+    get_service_namespaced_root,
+    get_service_namespaced_root_path,
+    join_paths,
+)
+
+from .goal_state_override import GoalStateOverride, OverrideProgress, OverrideStatus
+
+MAX_VALUE_LENGTH_BYTES = 1000 * 1000
+TASK_INFO_PATH_NAME = "TaskInfo"
+TASK_STATUS_PATH_NAME = "TaskStatus"
+TASK_METADATA_PATH_NAME = "Metadata"
+TASK_GOAL_OVERRIDE_PATH_NAME = "goal-state-override"
+TASK_GOAL_OVERRIDE_STATUS_PATH_NAME = "override-status"
+PROPERTIES_ROOT_NAME = "Properties"
+TASKS_ROOT_NAME = "Tasks"
+
+_NON_TERMINAL_OVERWRITE_STATES = frozenset(
+    [P.TASK_LOST, P.TASK_GONE, P.TASK_DROPPED, P.TASK_UNKNOWN, P.TASK_UNREACHABLE])
+
+
+class StateStoreException(Exception):
+    def __init__(self, reason: Reason, message: str = ""):
+        super().__init__(f"{reason.value}: {message}")
+        self.reason = reason
+
+
+class StateStore:
+    def __init__(self, persister: Persister, namespace: Optional[str] = None, repair: bool = True):
+        self.persister = persister
+        self.namespace = namespace or ""
+        self.logger = logging.getLogger(__name__ + (f"({self.namespace})" if self.namespace else ""))
+        if repair:
+            from .state_store_utils import repair_task_ids
+
+            repair_task_ids(self)
+
+    # -- paths ---------------------------------------------------------------------------
+    def _task_path(self, task_name: str) -> str:
+        return join_paths(get_service_namespaced_root_path(self.namespace, TASKS_ROOT_NAME), task_name)
+
+    def _task_info_path(self, name: str) -> str:
+        return join_paths(self._task_path(name), TASK_INFO_PATH_NAME)
+
+    def _task_status_path(self, name: str) -> str:
+        return join_paths(self._task_path(name), TASK_STATUS_PATH_NAME)
+
+    def _goal_override_path(self, name: str) -> str:
+        return join_paths(self._task_path(name), TASK_METADATA_PATH_NAME, TASK_GOAL_OVERRIDE_PATH_NAME)
+
+    def _goal_override_status_path(self, name: str) -> str:
+        return join_paths(self._task_path(name), TASK_METADATA_PATH_NAME, TASK_GOAL_OVERRIDE_STATUS_PATH_NAME)
+
+    def _property_path(self, key: str) -> str:
+        return join_paths(get_service_namespaced_root_path(self.namespace, PROPERTIES_ROOT_NAME), key)
+
+    @staticmethod
+    def _validate_key(key: str) -> None:
+        if not key or not key.strip():
+            raise StateStoreException(Reason.LOGIC_ERROR, "Key cannot be blank or null")
+        if "/" in key:
+            raise StateStoreException(Reason.LOGIC_ERROR, "Key cannot contain '/'")
+
+    @staticmethod
+    def _validate_value(value: Optional[bytes]) -> None:
+        if value is None:
+            raise StateStoreException(Reason.LOGIC_ERROR, "Property value must not be null.")
+        if len(value) > MAX_VALUE_LENGTH_BYTES:
+            raise StateStoreException(
+                Reason.LOGIC_ERROR,
+                f"Property value length {len(value)} exceeds limit of {MAX_VALUE_LENGTH_BYTES} bytes.")
+
+    # -- tasks ---------------------------------------------------------------------------
+    def store_tasks(self, tasks: Collection[P.TaskInfo]) -> None:
+        batches: List[Dict[str, bytes]] = []
+        sizes: List[int] = []
+        for t in tasks:
+            data = t.SerializeToString()
+            self._validate_value(data)
+            if not batches or len(data) + sizes[-1] >= MAX_VALUE_LENGTH_BYTES:
+                batches.append({})
+                sizes.append(0)
+            batches[-1][self._task_info_path(t.name)] = data
+            sizes[-1] += len(data)
+        if len(batches) > 1:
+            self.logger.warning("Grouped %d TaskInfo writes in to %d batches", len(tasks), len(batches))
+        for b in batches:
+            try:
+                self.persister.set_many(b)
+            except PersisterException as e:
+                raise StateStoreException(e.reason, f"Failed to store {len(b)} TaskInfos") from e
+
+    def store_status(self, task_name: str, status: P.TaskStatus) -> None:
+        current = self.fetch_status(task_name)
+        from dcos_commons_amd.offer.task_utils import is_terminal
+
+        if current is not None and status.state in _NON_TERMINAL_OVERWRITE_STATES and is_terminal(current):
+            raise StateStoreException(
+                Reason.LOGIC_ERROR,
+                f"Skipping task status processing. Ignoring {P.TaskState.Name(status.state)} as task already in a "
+                f"terminal state {P.TaskState.Name(current.state)}: {task_name}")
+        if (status.state != P.TASK_STAGING and current is not None
+                and current.task_id.value != status.task_id.value):
+            raise StateStoreException(Reason.NOT_FOUND,
+                                      f"Dropping TaskStatus with unknown TaskID: {status.task_id.value}")
+        try:
+            self.persister.set(self._task_status_path(task_name), status.SerializeToString())
+        except PersisterException as e:
+            raise StateStoreException(e.reason, str(e)) from e
+
+    def clear_task(self, task_name: str) -> None:
+        try:
+            self.persister.recursive_delete(self._task_path(task_name))
+        except PersisterException as e:
+            if e.reason == Reason.NOT_FOUND:
+                self.logger.warning("Cleared nonexistent Task, continuing silently: %s", task_name)
+            else:
+                raise StateStoreException(e.reason, str(e)) from e
+
+    def fetch_task_names(self) -> List[str]:
+        try:
+            return list(self.persister.get_children(
+                get_service_namespaced_root_path(self.namespace, TASKS_ROOT_NAME)))
+        except PersisterException as e:
+            if e.reason == Reason.NOT_FOUND:
+                return []
+            raise StateStoreException(e.reason, str(e)) from e
+
+    def fetch_tasks(self) -> List[P.TaskInfo]:
+        out = []
+        for name in self.fetch_task_names():
+            t = self.fetch_task(name)
+            if t is None:
+                raise StateStoreException(
+                    Reason.NOT_FOUND, f"Expected task named {name} to be present when retrieving all tasks")
+            out.append(t)
+        return out
+
+    def fetch_task(self, task_name: str) -> Optional[P.TaskInfo]:
+        try:
+            data = self.persister.get(self._task_info_path(task_name))
+        except PersisterException as e:
+            if e.reason == Reason.NOT_FOUND:
+                return None
+            raise StateStoreException(e.reason, f"Failed to retrieve task named {task_name}") from e
+        if not data:
+            raise StateStoreException(Reason.SERIALIZATION_ERROR, f"Empty TaskInfo for TaskName: {task_name}")
+        t = P.TaskInfo()
+        try:
+            t.ParseFromString(data)
+        except Exception as e:  # noqa: BLE001
+            raise StateStoreException(Reason.SERIALIZATION_ERROR, str(e)) from e
+        return t
+
+    def fetch_statuses(self) -> List[P.TaskStatus]:
+        out = []
+        for name in self.fetch_task_names():
+            try:
+                data = self.persister.get(self._task_status_path(name))
+            except PersisterException as e:
+                if e.reason == Reason.NOT_FOUND:
+                    continue
+                raise StateStoreException(e.reason, str(e)) from e
+            s = P.TaskStatus()
+            s.ParseFromString(data or b"")
+            out.append(s)
+        return out
+
+    def fetch_status(self, task_name: str) -> Optional[P.TaskStatus]:
+        try:
+            data = self.persister.get(self._task_status_path(task_name))
+        except PersisterException as e:
+            if e.reason == Reason.NOT_FOUND:
+                return None
+            raise StateStoreException(e.reason, str(e)) from e
+        if not data:
+            raise StateStoreException(Reason.SERIALIZATION_ERROR, f"Empty TaskStatus for TaskName: {task_name}")
+        s = P.TaskStatus()
+        s.ParseFromString(data)
+        return s
+
+    # -- properties ----------------------------------------------------------------------
+    def store_property(self, key: str, value: bytes) -> None:
+        self._validate_key(key)
+        self._validate_value(value)
+        try:
+            self.persister.set(self._property_path(key), value)
+        except PersisterException as e:
+            raise StateStoreException(e.reason, str(e)) from e
+
+    def store_properties(self, props: Dict[str, bytes]) -> None:
+        m = {}
+        for k, v in props.items():
+            self._validate_key(k)
+            self._validate_value(v)
+            m[self._property_path(k)] = v
+        try:
+            self.persister.set_many(m)
+        except PersisterException as e:
+            raise StateStoreException(e.reason, str(e)) from e
+
+    def fetch_property(self, key: str) -> bytes:
+        self._validate_key(key)
+        try:
+            return self.persister.get(self._property_path(key))
+        except PersisterException as e:
+            raise StateStoreException(e.reason, str(e)) from e
+
+    def fetch_property_keys(self) -> List[str]:
+        try:
+            return list(self.persister.get_children(
+                get_service_namespaced_root_path(self.namespace, PROPERTIES_ROOT_NAME)))
+        except PersisterException as e:
+            if e.reason == Reason.NOT_FOUND:
+                return []
+            raise StateStoreException(e.reason, str(e)) from e
+
+    def clear_property(self, key: str) -> None:
+        self._validate_key(key)
+        try:
+            self.persister.recursive_delete(self._property_path(key))
+        except PersisterException as e:
+            if e.reason != Reason.NOT_FOUND:
+                raise StateStoreException(e.reason, str(e)) from e
+
+    # -- goal overrides ------------------------------------------------------------------
+    def store_goal_override_status(self, task_name: str, status: OverrideStatus) -> None:
+        try:
+            if status == OverrideStatus.INACTIVE:
+                self.persister.recursive_delete_many(
+                    [self._goal_override_path(task_name), self._goal_override_status_path(task_name)])
+            else:
+                self.persister.set_many({
+                    self._goal_override_path(task_name): status.target.serialized_name.encode(),
+                    self._goal_override_status_path(task_name): status.progress.value.encode(),
+                })
+        except PersisterException as e:
+            raise StateStoreException(e.reason, str(e)) from e
+
+    def fetch_goal_override_status(self, task_name: str) -> OverrideStatus:
+        p1, p2 = self._goal_override_path(task_name), self._goal_override_status_path(task_name)
+        try:
+            vals = self.persister.get_many([p1, p2])
+        except PersisterException as e:
+            raise StateStoreException(e.reason, str(e)) from e
+        name_b, prog_b = vals.get(p1), vals.get(p2)
+        if name_b is None and prog_b is None:
+            return OverrideStatus.INACTIVE
+        if name_b is None or prog_b is None:
+            self.logger.error("Task %s is missing override name or override status", task_name)
+            return OverrideStatus.INACTIVE
+        target = GoalStateOverride.from_serialized(name_b.decode())
+        if target is None:
+            return OverrideStatus.INACTIVE
+        try:
+            progress = OverrideProgress(prog_b.decode())
+        except ValueError:
+            return OverrideStatus.INACTIVE
+        return OverrideStatus(target, progress)
+
+    def delete_all_data_if_namespaced(self) -> None:
+        if not self.namespace:
+            return
+        try:
+            self.persister.recursive_delete(get_service_namespaced_root(self.namespace))
+        except PersisterException as e:
+            if e.reason != Reason.NOT_FOUND:
+                raise StateStoreException(e.reason, str(e)) from e
