@@ -25,6 +25,7 @@ class Capabilities:
     supports_shm: bool = True
     supports_domains: bool = True
     supports_v1_api_by_default: bool = True
+    supports_partition_awareness: bool = True
     version: str = "1.13"
 
     def with_overrides(self, **kw) -> "Capabilities":

@@ -1,0 +1,173 @@
+"""Mesos callback sink for one framework.
+
+Reference: sdk/.../framework/FrameworkScheduler.java:42-300. Stores the FrameworkID on first
+registration, installs the driver and the master's domain, starts the offer processor and the
+implicit reconciler, drops offers until the API server is up (short decline), strips resources
+that belong to other frameworks/roles, routes status updates to the client and kills tasks it
+does not know, and exits the process on disconnect/error.
+"""
+from __future__ import annotations
+
+import logging
+import threading
+
+from dcos_commons_amd import metrics
+from dcos_commons_amd.mesos import protos as P
+from dcos_commons_amd.offer import resources as ResourceUtils
+from dcos_commons_amd.offer.evaluate.placement import IsLocalRegionRule
+from dcos_commons_amd.scheduler.mesos_event_client import TaskStatusResult
+from dcos_commons_amd.state.state_store import StateStoreException
+
+from . import driver as driver_mod
+from . import task_killer
+from .offer_processing import ImplicitReconciler, OfferProcessor, TokenBucket, decline_short
+from .process_exit import ProcessExit
+
+LOGGER = logging.getLogger(__name__)
+
+
+class FrameworkScheduler:
+    def __init__(self, roles_whitelist, scheduler_config, persister, framework_store, client,
+                 offer_processor: OfferProcessor = None, implicit_reconciler: ImplicitReconciler = None):
+        self.roles_whitelist = set(roles_whitelist)
+        self.framework_store = framework_store
+        self.client = client
+        self.offer_processor = offer_processor or OfferProcessor(
+            client, persister, scheduler_config,
+            token_bucket=TokenBucket(acquire_interval_s=scheduler_config.revive_interval_s())
+            if scheduler_config is not None else None,
+            hold_s=scheduler_config.offer_hold_s() if scheduler_config is not None else 0.0,
+            event_driven=scheduler_config.is_event_driven() if scheduler_config is not None else False)
+        if implicit_reconciler is None:
+            implicit_reconciler = ImplicitReconciler(
+                scheduler_config.implicit_reconcile_delay_s() if scheduler_config is not None else 0.0,
+                scheduler_config.implicit_reconcile_period_s() if scheduler_config is not None else 3600.0)
+        self.implicit_reconciler = implicit_reconciler
+        self._register_called = False
+        self._api_server_started = threading.Event()
+        self._lock = threading.Lock()
+
+    # -- configuration ---------------------------------------------------------------
+    def set_api_server_started(self) -> "FrameworkScheduler":
+        self._api_server_started.set()
+        return self
+
+    def disable_threading(self) -> "FrameworkScheduler":
+        self.offer_processor.disable_threading()
+        self.implicit_reconciler.disable_threading()
+        return self
+
+    def set_revive_token_bucket(self, bucket) -> "FrameworkScheduler":
+        self.offer_processor.set_revive_token_bucket(bucket)
+        return self
+
+    @staticmethod
+    def _exit(e: BaseException) -> None:
+        LOGGER.error("Got exception when invoked by Mesos, shutting down.", exc_info=e)
+        ProcessExit.exit(ProcessExit.ERROR, e)
+
+    @staticmethod
+    def _update_driver_and_domain(driver, master_info) -> None:
+        driver_mod.set_driver(driver)
+        if master_info is not None and master_info.HasField("domain"):
+            IsLocalRegionRule.set_local_domain(master_info.domain)
+
+    # -- Mesos callbacks ---------------------------------------------------------------
+    def registered(self, driver, framework_id: P.FrameworkID, master_info) -> None:
+        try:
+            with self._lock:
+                again = self._register_called
+                self._register_called = True
+            if again:
+                self.reregistered(driver, master_info)
+                return
+            try:
+                self.framework_store.store_framework_id(framework_id)
+            except StateStoreException as e:
+                LOGGER.error("Unable to store registered framework ID '%s'", framework_id.value)
+                ProcessExit.exit(ProcessExit.REGISTRATION_FAILURE, e)
+            self._update_driver_and_domain(driver, master_info)
+            self.client.registered(False)
+            self.offer_processor.start()
+            self.implicit_reconciler.start()
+        except Exception as e:  # noqa: BLE001
+            self._exit(e)
+
+    def reregistered(self, driver, master_info) -> None:
+        try:
+            self._update_driver_and_domain(driver, master_info)
+            self.client.registered(True)
+        except Exception as e:  # noqa: BLE001
+            self._exit(e)
+
+    def resource_offers(self, driver, offers) -> None:
+        try:
+            metrics.increment_received_offers(len(offers))
+            if not self._api_server_started.is_set():
+                LOGGER.info("Declining %d offer%s: Waiting for API server to start.", len(offers),
+                            "" if len(offers) == 1 else "s")
+                decline_short(offers)
+                return
+            fid = self.framework_store.fetch_framework_id()
+            fid = fid.value if fid is not None else None
+            self.offer_processor.enqueue([self._filter_bad_resources(o, fid) for o in offers])
+        except Exception as e:  # noqa: BLE001
+            self._exit(e)
+
+    def _filter_bad_resources(self, offer: P.Offer, framework_id) -> P.Offer:
+        good = [r for r in offer.resources if ResourceUtils.is_processable(r, self.roles_whitelist, framework_id)]
+        if len(good) == len(offer.resources):
+            return offer
+        LOGGER.info("Filtered %d resources from offer %s", len(offer.resources) - len(good), offer.id.value)
+        out = P.Offer()
+        out.CopyFrom(offer)
+        del out.resources[:]
+        out.resources.extend(good)
+        return out
+
+    def status_update(self, driver, status: P.TaskStatus) -> None:
+        try:
+            LOGGER.info("Received status update for taskId=%s state=%s message='%s'", status.task_id.value,
+                        P.TaskState.Name(status.state), status.message)
+            metrics.record_status(status)
+            resp = self.client.task_status(status)
+            eligible = task_killer.update(status)
+            if resp.result == TaskStatusResult.UNKNOWN_TASK:
+                if eligible:
+                    LOGGER.info("Received status update for unknown task, marking task to be killed: %s",
+                                status.task_id.value)
+                    task_killer.kill_task(status.task_id)
+                else:
+                    LOGGER.warning("Received status update for unknown task, but task should not be killed "
+                                   "again: %s", status.task_id.value)
+            self.offer_processor.kick()
+        except Exception as e:  # noqa: BLE001
+            self._exit(e)
+
+    def offer_rescinded(self, driver, offer_id: P.OfferID) -> None:
+        try:
+            self.offer_processor.dequeue(offer_id)
+        except Exception as e:  # noqa: BLE001
+            self._exit(e)
+
+    def framework_message(self, driver, executor_id, agent_id, data: bytes) -> None:
+        LOGGER.error("Received unsupported %d byte Framework Message from Executor %s on Agent %s", len(data),
+                     executor_id.value, agent_id.value)
+
+    def disconnected(self, driver) -> None:
+        LOGGER.error("Disconnected from Master, shutting down.")
+        ProcessExit.exit(ProcessExit.DISCONNECTED)
+
+    def agent_lost(self, driver, agent_id) -> None:
+        LOGGER.warning("Agent lost: %s", agent_id.value)
+
+    def executor_lost(self, driver, executor_id, agent_id, status: int) -> None:
+        LOGGER.warning("Lost Executor: %s on Agent: %s", executor_id.value, agent_id.value)
+
+    def error(self, driver, message: str) -> None:
+        LOGGER.error("SchedulerDriver returned an error, shutting down: %s", message)
+        ProcessExit.exit(ProcessExit.ERROR)
+
+    def stop(self) -> None:
+        self.offer_processor.stop()
+        self.implicit_reconciler.stop()

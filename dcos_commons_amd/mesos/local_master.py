@@ -1,0 +1,877 @@
+"""An in-process Mesos master + agents with a scheduler driver.
+
+This is the cluster the scheduler talks to in tests, the simulation harness and the benchmark
+(the reference talks to a real Mesos master through libmesos; none exists here). It models what
+the SDK's timing and correctness depend on:
+
+* **allocation** -- every ``allocation_interval_s`` (Mesos ``--allocation_interval``, default
+  1 s) each subscribed, unsuppressed framework is offered the unreserved + role-reserved
+  resources of every agent that has no outstanding offer and no active decline filter; REVIVE
+  clears filters and triggers an immediate allocation;
+* **offer operations** -- RESERVE / UNRESERVE / CREATE / DESTROY / LAUNCH_GROUP applied in
+  order on the offered resources (``resource_math.ResourceBag``); leftovers go back to the agent
+  with the ACCEPT's ``refuse_seconds`` filter;
+* **task lifecycle** -- STAGING -> STARTING -> RUNNING (with an empty ``check_status`` when the
+  task has a check, then ``exit_code`` once the readiness check passes, honouring
+  ``delay_seconds``) -> terminal; KILL -> KILLED; executor resources are released when its last
+  task ends; GPUs are assigned by device index (``HIP_VISIBLE_DEVICES`` for the task);
+* **reconciliation** (implicit and explicit), **teardown**, **agent loss** and fault injection
+  (``fail_task``, ``lose_agent``) for recovery/MTTR measurements.
+
+All state is owned by one dispatcher thread (an actor): driver calls and test hooks enqueue
+actions, and scheduler callbacks are delivered from that thread in order.
+"""
+from __future__ import annotations
+
+import heapq
+import itertools
+import logging
+import threading
+import time
+import uuid
+from concurrent.futures import Future
+from dataclasses import dataclass, field
+from typing import Callable, Dict, List, Optional, Set, Tuple
+
+from dcos_commons_amd.framework.driver import SchedulerDriver
+from dcos_commons_amd.mesos import protos as P
+from dcos_commons_amd.mesos.resource_math import (
+    InsufficientResources,
+    ResourceBag,
+    effective_role,
+    pop_reservation,
+    strip_volume,
+)
+
+LOGGER = logging.getLogger(__name__)
+TERMINAL = {P.TASK_FINISHED, P.TASK_FAILED, P.TASK_KILLED, P.TASK_ERROR, P.TASK_LOST, P.TASK_DROPPED,
+            P.TASK_GONE, P.TASK_GONE_BY_OPERATOR}
+
+
+def scalar(name: str, value: float) -> P.Resource:
+    r = P.Resource(name=name, type=P.Value.SCALAR)
+    r.scalar.value = value
+    return r
+
+
+def ranges(name: str, intervals) -> P.Resource:
+    r = P.Resource(name=name, type=P.Value.RANGES)
+    r.ranges.SetInParent()
+    for b, e in intervals:
+        r.ranges.range.add(begin=b, end=e)
+    return r
+
+
+def text_attribute(name: str, value: str) -> P.Attribute:
+    a = P.Attribute(name=name, type=P.Value.TEXT)
+    a.text.value = value
+    return a
+
+
+@dataclass
+class AgentSpec:
+    hostname: str
+    cpus: float = 8.0
+    mem: float = 32768.0
+    disk: float = 65536.0
+    ports: Tuple[Tuple[int, int], ...] = ((10000, 20000),)
+    gpus: int = 0
+    gpu_devices: Optional[List[int]] = None  # physical device indices; default range(gpus)
+    attributes: Dict[str, str] = field(default_factory=dict)
+    zone: Optional[str] = None
+    region: Optional[str] = None
+    mount_disks: Tuple[Tuple[str, float], ...] = ()
+    pre_reserved: Tuple[Tuple[str, str, float], ...] = ()  # (role, resource name, amount)
+
+    def resources(self) -> List[P.Resource]:
+        out = []
+        for name, amount in (("cpus", self.cpus), ("mem", self.mem), ("disk", self.disk)):
+            if amount > 0:
+                out.append(scalar(name, amount))
+        if self.ports:
+            out.append(ranges("ports", self.ports))
+        if self.gpus:
+            out.append(scalar("gpus", float(self.gpus)))
+        for root, size in self.mount_disks:
+            r = scalar("disk", size)
+            r.disk.source.type = P.Resource.DiskInfo.Source.MOUNT
+            r.disk.source.mount.root = root
+            out.append(r)
+        # statically pre-reserved resources come out of the unreserved pool
+        bag = ResourceBag(out)
+        for role, name, amount in self.pre_reserved:
+            bag.subtract(scalar(name, amount))
+            r = scalar(name, amount)
+            r.reservations.add(type=P.Resource.ReservationInfo.STATIC, role=role)
+            bag.add(r)
+        return bag.to_resources()
+
+    def domain(self) -> Optional[P.DomainInfo]:
+        if not self.zone and not self.region:
+            return None
+        d = P.DomainInfo()
+        d.fault_domain.region.name = self.region or "default-region"
+        d.fault_domain.zone.name = self.zone or "default-zone"
+        return d
+
+
+@dataclass
+class TaskTiming:
+    """Synthetic task lifecycle timing (seconds after the previous event)."""
+    starting_s: float = 0.0
+    running_s: float = 0.0
+    honor_check_delays: bool = True
+    check_exec_s: float = 0.0
+    finish_after_s: Optional[float] = None  # None: runs until killed
+    exit_state: int = P.TASK_FINISHED
+
+
+class TaskBehavior:
+    """Decides the synthetic lifecycle of a launched task; override ``timing`` for scenarios."""
+
+    def __init__(self, default: Optional[TaskTiming] = None,
+                 overrides: Optional[Dict[str, TaskTiming]] = None):
+        self.default = default or TaskTiming()
+        self.overrides = dict(overrides or {})
+
+    def timing(self, task: P.TaskInfo) -> TaskTiming:
+        for k, v in self.overrides.items():
+            if k in task.name:
+                return v
+        return self.default
+
+
+@dataclass
+class _Task:
+    info: P.TaskInfo
+    framework_id: str
+    executor_id: str
+    agent_id: str
+    resources: List[P.Resource]
+    gpu_devices: List[int]
+    status: P.TaskStatus
+    epoch: int = 0  # bumps on kill/failure so stale timers are ignored
+
+
+@dataclass
+class _Executor:
+    info: P.ExecutorInfo
+    framework_id: str
+    resources: List[P.Resource]
+    tasks: Set[str] = field(default_factory=set)
+
+
+class _Agent:
+    def __init__(self, agent_id: str, spec: AgentSpec):
+        self.id = agent_id
+        self.spec = spec
+        self.available = ResourceBag(spec.resources())
+        self.executors: Dict[Tuple[str, str], _Executor] = {}
+        self.tasks: Dict[str, _Task] = {}
+        devices = spec.gpu_devices if spec.gpu_devices is not None else list(range(spec.gpus))
+        self.free_gpus: List[int] = list(devices)
+        self.active = True
+
+    def info_attributes(self) -> List[P.Attribute]:
+        return [text_attribute(k, v) for k, v in sorted(self.spec.attributes.items())]
+
+
+@dataclass
+class _Framework:
+    id: str
+    info: P.FrameworkInfo
+    driver: "LocalSchedulerDriver"
+    roles: Set[str]
+    suppressed: bool = False
+    connected: bool = True
+    filters: Dict[str, float] = field(default_factory=dict)  # agent id -> filter expiry
+
+
+@dataclass
+class _Offer:
+    id: str
+    framework_id: str
+    agent_id: str
+    resources: List[P.Resource]
+
+
+class LocalMaster:
+    def __init__(self, allocation_interval_s: float = 1.0, behavior: Optional[TaskBehavior] = None,
+                 domain: Optional[P.DomainInfo] = None, offer_timeout_s: Optional[float] = None,
+                 clock: Callable[[], float] = time.monotonic):
+        self.allocation_interval_s = allocation_interval_s
+        self.behavior = behavior or TaskBehavior()
+        self.domain = domain
+        self.offer_timeout_s = offer_timeout_s
+        self.clock = clock
+        self.master_info = P.MasterInfo(id="local-master-" + uuid.uuid4().hex[:8], hostname="127.0.0.1",
+                                        version="1.9.0-local")
+        if domain is not None:
+            self.master_info.domain.CopyFrom(domain)
+        self.agents: Dict[str, _Agent] = {}
+        self.frameworks: Dict[str, _Framework] = {}
+        self.offers: Dict[str, _Offer] = {}
+        self._seq = itertools.count()
+        self._heap: List[tuple] = []
+        self._cond = threading.Condition()
+        self._running = True
+        self._thread = threading.Thread(target=self._run, name="LocalMaster", daemon=True)
+        self._listeners: List[Callable[[str, P.TaskStatus], None]] = []
+        self.accept_calls = 0
+        self.operations: List[Tuple[str, int]] = []  # (agent id, operation type) in applied order
+        self._thread.start()
+        self._schedule(self.allocation_interval_s, self._periodic_allocate)
+
+    # -- actor plumbing ----------------------------------------------------------------
+    def _schedule(self, delay: float, fn, *args) -> None:
+        with self._cond:
+            heapq.heappush(self._heap, (self.clock() + max(0.0, delay), next(self._seq), fn, args))
+            self._cond.notify()
+
+    def _run(self) -> None:
+        while True:
+            with self._cond:
+                while self._running and (not self._heap or self._heap[0][0] > self.clock()):
+                    timeout = None if not self._heap else max(0.0, self._heap[0][0] - self.clock())
+                    self._cond.wait(timeout if timeout is None else min(timeout, 0.5))
+                if not self._running:
+                    return
+                _, _, fn, args = heapq.heappop(self._heap)
+            try:
+                fn(*args)
+            except Exception:  # noqa: BLE001
+                LOGGER.exception("LocalMaster action %s failed", getattr(fn, "__name__", fn))
+
+    def call(self, fn, *args, timeout: float = 30.0):
+        """Run ``fn`` on the dispatcher thread and return its result (test hooks/queries)."""
+        if threading.current_thread() is self._thread:
+            return fn(*args)
+        fut: Future = Future()
+
+        def run():
+            try:
+                fut.set_result(fn(*args))
+            except Exception as e:  # noqa: BLE001
+                fut.set_exception(e)
+        self._schedule(0, run)
+        return fut.result(timeout)
+
+    def shutdown(self) -> None:
+        with self._cond:
+            self._running = False
+            self._cond.notify_all()
+        if threading.current_thread() is not self._thread:
+            self._thread.join(timeout=5)
+
+    def add_status_listener(self, fn: Callable[[str, P.TaskStatus], None]) -> None:
+        self._listeners.append(fn)
+
+    # -- cluster management --------------------------------------------------------------
+    def add_agent(self, spec: AgentSpec) -> str:
+        def do():
+            aid = f"agent-{len(self.agents)}-{uuid.uuid4().hex[:6]}"
+            self.agents[aid] = _Agent(aid, spec)
+            self._allocate()
+            return aid
+        return self.call(do)
+
+    def lose_agent(self, agent_id: str, partition_aware: bool = True) -> None:
+        """Agent disappears: outstanding offers are rescinded and its tasks go UNREACHABLE/LOST."""
+        def do():
+            a = self.agents[agent_id]
+            a.active = False
+            for oid in [o.id for o in self.offers.values() if o.agent_id == agent_id]:
+                self._rescind(oid)
+            for t in list(a.tasks.values()):
+                if t.status.state in TERMINAL:
+                    continue
+                fw = self.frameworks.get(t.framework_id)
+                aware = partition_aware and fw is not None and any(
+                    c.type == P.FrameworkInfo.Capability.PARTITION_AWARE for c in fw.info.capabilities)
+                self._update(t, P.TASK_UNREACHABLE if aware else P.TASK_LOST, source=P.TaskStatus.SOURCE_MASTER,
+                             reason=P.TaskStatus.REASON_AGENT_REMOVED, message="Agent lost")
+        self.call(do)
+
+    def fail_task(self, task_id: str, state: int = P.TASK_FAILED, message: str = "injected failure") -> None:
+        def do():
+            t = self._find_task(task_id)
+            if t is None:
+                raise KeyError(task_id)
+            self._update(t, state, message=message, reason=P.TaskStatus.REASON_COMMAND_EXECUTOR_FAILED)
+        self.call(do)
+
+    def send_status(self, task_id: str, state: int, **fields) -> None:
+        def do():
+            t = self._find_task(task_id)
+            self._update(t, state, **fields)
+        self.call(do)
+
+    def task_states(self, framework_id: Optional[str] = None) -> Dict[str, int]:
+        def do():
+            out = {}
+            for a in self.agents.values():
+                for tid, t in a.tasks.items():
+                    if framework_id is None or t.framework_id == framework_id:
+                        out[tid] = t.status.state
+            return out
+        return self.call(do)
+
+    def tasks_by_name(self, include_terminal: bool = False) -> Dict[str, P.TaskInfo]:
+        def do():
+            out = {}
+            for a in self.agents.values():
+                for t in a.tasks.values():
+                    if include_terminal or t.status.state not in TERMINAL:
+                        out[t.info.name] = t.info
+            return out
+        return self.call(do)
+
+    def agent_resources(self, agent_id: str) -> List[P.Resource]:
+        return self.call(lambda: self.agents[agent_id].available.to_resources())
+
+    def reserved_resources(self, agent_id: str) -> List[P.Resource]:
+        def do():
+            a = self.agents[agent_id]
+            rs = a.available.to_resources()
+            for o in self.offers.values():
+                if o.agent_id == agent_id:
+                    rs.extend(o.resources)
+            for e in a.executors.values():
+                rs.extend(e.resources)
+            for t in a.tasks.values():
+                if t.status.state not in TERMINAL:
+                    rs.extend(t.resources)
+            return [r for r in rs if len(r.reservations) and
+                    r.reservations[-1].type == P.Resource.ReservationInfo.DYNAMIC]
+        return self.call(do)
+
+    # -- framework-facing API (called through LocalSchedulerDriver) -------------------------
+    def subscribe(self, driver: "LocalSchedulerDriver", info: P.FrameworkInfo) -> None:
+        def do():
+            fid = info.id.value if info.HasField("id") and info.id.value else "fw-" + uuid.uuid4().hex
+            roles = set(info.roles) if len(info.roles) else {info.role or "*"}
+            existing = self.frameworks.get(fid)
+            fw = _Framework(fid, info, driver, roles)
+            if existing is not None:
+                fw.filters = {}
+            self.frameworks[fid] = fw
+            driver._framework_id = fid
+            driver._deliver(lambda s: s.registered(driver, P.FrameworkID(value=fid), self.master_info))
+            self._allocate()
+        self._schedule(0, do)
+
+    def _fw(self, fid: str) -> Optional[_Framework]:
+        fw = self.frameworks.get(fid)
+        return fw if fw is not None and fw.connected else None
+
+    def accept(self, fid: str, offer_ids: List[str], ops: List[P.Offer.Operation], refuse_s: float) -> None:
+        self._schedule(0, self._accept, fid, list(offer_ids), list(ops), refuse_s)
+
+    def decline(self, fid: str, offer_ids: List[str], refuse_s: float) -> None:
+        self._schedule(0, self._decline, fid, list(offer_ids), refuse_s)
+
+    def revive(self, fid: str) -> None:
+        def do():
+            fw = self._fw(fid)
+            if fw is None:
+                return
+            fw.suppressed = False
+            fw.filters.clear()
+            self._allocate()
+        self._schedule(0, do)
+
+    def suppress(self, fid: str) -> None:
+        def do():
+            fw = self._fw(fid)
+            if fw is not None:
+                fw.suppressed = True
+        self._schedule(0, do)
+
+    def kill(self, fid: str, task_id: str) -> None:
+        self._schedule(0, self._kill, fid, task_id)
+
+    def reconcile(self, fid: str, statuses: List[P.TaskStatus]) -> None:
+        self._schedule(0, self._reconcile, fid, list(statuses))
+
+    def teardown(self, fid: str) -> None:
+        def do():
+            fw = self.frameworks.get(fid)
+            if fw is None:
+                return
+            fw.connected = False
+            for oid in [o.id for o in self.offers.values() if o.framework_id == fid]:
+                self._return_offer(oid, 0)
+            for a in self.agents.values():
+                for t in list(a.tasks.values()):
+                    if t.framework_id == fid and t.status.state not in TERMINAL:
+                        self._update(t, P.TASK_KILLED, reason=P.TaskStatus.REASON_FRAMEWORK_REMOVED, deliver=False)
+            del self.frameworks[fid]
+        self._schedule(0, do)
+
+    def disconnect(self, fid: str) -> None:
+        def do():
+            fw = self.frameworks.get(fid)
+            if fw is None:
+                return
+            fw.connected = False
+            for oid in [o.id for o in self.offers.values() if o.framework_id == fid]:
+                self._return_offer(oid, 0)
+        self._schedule(0, do)
+
+    # -- allocation -------------------------------------------------------------------
+    def _periodic_allocate(self) -> None:
+        self._allocate()
+        if self._running:
+            self._schedule(self.allocation_interval_s, self._periodic_allocate)
+
+    def _offerable(self, fw: _Framework, r: P.Resource) -> bool:
+        role = effective_role(r)
+        return role == "*" or role in fw.roles
+
+    def _allocate(self) -> None:
+        now = self.clock()
+        for fw in list(self.frameworks.values()):
+            if not fw.connected or fw.suppressed:
+                continue
+            batch: List[P.Offer] = []
+            for a in self.agents.values():
+                if not a.active:
+                    continue
+                if any(o.agent_id == a.id and o.framework_id == fw.id for o in self.offers.values()):
+                    continue
+                exp = fw.filters.get(a.id)
+                if exp is not None:
+                    if exp > now:
+                        continue
+                    del fw.filters[a.id]
+                mine = [r for r in a.available.to_resources() if self._offerable(fw, r)]
+                if not mine:
+                    continue
+                for r in mine:
+                    a.available.subtract(r)
+                alloc_role = sorted(fw.roles)[0]
+                for r in mine:
+                    role = effective_role(r)
+                    r.allocation_info.role = role if role != "*" else alloc_role
+                oid = "offer-" + uuid.uuid4().hex
+                self.offers[oid] = _Offer(oid, fw.id, a.id, mine)
+                o = P.Offer(hostname=a.spec.hostname)
+                o.id.value = oid
+                o.framework_id.value = fw.id
+                o.agent_id.value = a.id
+                o.resources.extend(mine)
+                o.attributes.extend(a.info_attributes())
+                d = a.spec.domain()
+                if d is not None:
+                    o.domain.CopyFrom(d)
+                for (efid, eid), e in a.executors.items():
+                    if efid == fw.id:
+                        o.executor_ids.add(value=eid)
+                batch.append(o)
+                if self.offer_timeout_s:
+                    self._schedule(self.offer_timeout_s, self._expire_offer, oid)
+            if batch:
+                fw.driver._deliver(lambda s, b=batch, d=fw.driver: s.resource_offers(d, b))
+
+    def _expire_offer(self, oid: str) -> None:
+        if oid in self.offers:
+            self._rescind(oid)
+
+    def _rescind(self, oid: str) -> None:
+        o = self.offers.get(oid)
+        if o is None:
+            return
+        self._return_offer(oid, 0)
+        fw = self.frameworks.get(o.framework_id)
+        if fw is not None and fw.connected:
+            fw.driver._deliver(lambda s, d=fw.driver: s.offer_rescinded(d, P.OfferID(value=oid)))
+
+    def _return_offer(self, oid: str, refuse_s: float, leftover: Optional[ResourceBag] = None) -> None:
+        o = self.offers.pop(oid, None)
+        if o is None:
+            return
+        a = self.agents.get(o.agent_id)
+        if a is None:
+            return
+        rs = leftover.take_all() if leftover is not None else o.resources
+        for r in rs:
+            r.ClearField("allocation_info")
+            a.available.add(r)
+        fw = self.frameworks.get(o.framework_id)
+        if fw is not None and refuse_s > 0:
+            fw.filters[o.agent_id] = max(fw.filters.get(o.agent_id, 0.0), self.clock() + refuse_s)
+
+    def _decline(self, fid: str, offer_ids: List[str], refuse_s: float) -> None:
+        for oid in offer_ids:
+            o = self.offers.get(oid)
+            if o is not None and o.framework_id == fid:
+                self._return_offer(oid, refuse_s)
+
+    # -- ACCEPT -----------------------------------------------------------------------
+    def _accept(self, fid: str, offer_ids: List[str], ops: List[P.Offer.Operation], refuse_s: float) -> None:
+        self.accept_calls += 1
+        fw = self._fw(fid)
+        offers = [self.offers.get(oid) for oid in offer_ids]
+        if fw is None or not offers or any(o is None or o.framework_id != fid for o in offers) or \
+                len({o.agent_id for o in offers}) != 1:
+            # invalid offers: every launched task is dropped
+            for op in ops:
+                for t in self._op_tasks(op):
+                    self._deliver_synthetic(fid, t, P.TASK_DROPPED, P.TaskStatus.REASON_INVALID_OFFERS,
+                                            "Offers are invalid or no longer valid")
+            return
+        agent = self.agents[offers[0].agent_id]
+        bag = ResourceBag()
+        for o in offers:
+            for r in o.resources:
+                c = P.Resource()
+                c.CopyFrom(r)
+                c.ClearField("allocation_info")
+                bag.add(c)
+        for op in ops:
+            self.operations.append((agent.id, op.type))
+            try:
+                self._apply(fw, agent, bag, op)
+            except InsufficientResources as e:
+                LOGGER.warning("Operation %s failed on %s: %s", P.Offer.Operation.Type.Name(op.type), agent.id, e)
+                for t in self._op_tasks(op):
+                    self._deliver_synthetic(fid, t, P.TASK_ERROR, P.TaskStatus.REASON_TASK_INVALID, str(e))
+        # first offer returns the leftovers; the others are simply consumed
+        for i, oid in enumerate(offer_ids):
+            if i == 0:
+                self._return_offer(oid, refuse_s, leftover=bag)
+            else:
+                self.offers.pop(oid, None)
+
+    @staticmethod
+    def _op_tasks(op: P.Offer.Operation) -> List[P.TaskInfo]:
+        if op.type == P.Offer.Operation.LAUNCH_GROUP:
+            return list(op.launch_group.task_group.tasks)
+        if op.type == P.Offer.Operation.LAUNCH:
+            return list(op.launch.task_infos)
+        return []
+
+    def _apply(self, fw: _Framework, agent: _Agent, bag: ResourceBag, op: P.Offer.Operation) -> None:
+        T = P.Offer.Operation
+        if op.type == T.RESERVE:
+            trial = bag.copy()
+            for r in op.reserve.resources:
+                trial.subtract(pop_reservation(r))
+                c = P.Resource()
+                c.CopyFrom(r)
+                c.ClearField("allocation_info")
+                trial.add(c)
+            bag._q, bag._proto = trial._q, trial._proto
+        elif op.type == T.UNRESERVE:
+            trial = bag.copy()
+            for r in op.unreserve.resources:
+                c = P.Resource()
+                c.CopyFrom(r)
+                c.ClearField("allocation_info")
+                trial.subtract(c)
+                trial.add(pop_reservation(c))
+            bag._q, bag._proto = trial._q, trial._proto
+        elif op.type == T.CREATE:
+            trial = bag.copy()
+            for v in op.create.volumes:
+                trial.subtract(strip_volume(v))
+                c = P.Resource()
+                c.CopyFrom(v)
+                c.ClearField("allocation_info")
+                trial.add(c)
+            bag._q, bag._proto = trial._q, trial._proto
+        elif op.type == T.DESTROY:
+            trial = bag.copy()
+            for v in op.destroy.volumes:
+                c = P.Resource()
+                c.CopyFrom(v)
+                c.ClearField("allocation_info")
+                trial.subtract(c)
+                trial.add(strip_volume(c))
+            bag._q, bag._proto = trial._q, trial._proto
+        elif op.type == T.LAUNCH_GROUP:
+            self._launch_group(fw, agent, bag, op.launch_group.executor, list(op.launch_group.task_group.tasks))
+        elif op.type == T.LAUNCH:
+            for t in op.launch.task_infos:
+                self._launch_group(fw, agent, bag, t.executor if t.HasField("executor") else None, [t])
+        else:
+            raise InsufficientResources(f"unsupported operation {op.type}")
+
+    @staticmethod
+    def _clean(rs) -> List[P.Resource]:
+        out = []
+        for r in rs:
+            c = P.Resource()
+            c.CopyFrom(r)
+            c.ClearField("allocation_info")
+            out.append(c)
+        return out
+
+    def _launch_group(self, fw: _Framework, agent: _Agent, bag: ResourceBag, executor: Optional[P.ExecutorInfo],
+                      tasks: List[P.TaskInfo]) -> None:
+        trial = bag.copy()
+        eid = executor.executor_id.value if executor is not None else ""
+        key = (fw.id, eid)
+        new_exec = executor is not None and key not in agent.executors
+        exec_rs = self._clean(executor.resources) if new_exec else []
+        trial.subtract_all(exec_rs)
+        per_task = []
+        for t in tasks:
+            rs = self._clean(t.resources)
+            trial.subtract_all(rs)
+            per_task.append(rs)
+        gpus_needed = [int(round(sum(r.scalar.value for r in rs if r.name == "gpus"))) for rs in per_task]
+        if sum(gpus_needed) > len(agent.free_gpus):
+            raise InsufficientResources("not enough free GPU devices")
+        bag._q, bag._proto = trial._q, trial._proto
+        if new_exec:
+            agent.executors[key] = _Executor(executor, fw.id, exec_rs)
+        for t, rs, ng in zip(tasks, per_task, gpus_needed):
+            devices = [agent.free_gpus.pop(0) for _ in range(ng)]
+            st = P.TaskStatus(state=P.TASK_STAGING, source=P.TaskStatus.SOURCE_MASTER, timestamp=time.time())
+            st.task_id.CopyFrom(t.task_id)
+            st.agent_id.value = agent.id
+            if eid:
+                st.executor_id.value = eid
+            task = _Task(t, fw.id, eid, agent.id, rs, devices, st)
+            agent.tasks[t.task_id.value] = task
+            if eid:
+                agent.executors[key].tasks.add(t.task_id.value)
+            timing = self.behavior.timing(t)
+            self._schedule(timing.starting_s, self._lifecycle_starting, task, task.epoch, timing)
+
+    # -- task lifecycle ----------------------------------------------------------------
+    def _lifecycle_starting(self, task: _Task, epoch: int, timing: TaskTiming) -> None:
+        if task.epoch != epoch or task.status.state in TERMINAL:
+            return
+        self._update(task, P.TASK_STARTING)
+        self._schedule(timing.running_s, self._lifecycle_running, task, epoch, timing)
+
+    def _lifecycle_running(self, task: _Task, epoch: int, timing: TaskTiming) -> None:
+        if task.epoch != epoch or task.status.state in TERMINAL:
+            return
+        extra = {}
+        info = task.info
+        if info.HasField("check"):
+            cs = P.CheckStatusInfo(type=info.check.type)
+            cs.command.SetInParent()
+            extra["check_status"] = cs
+        if info.HasField("health_check"):
+            extra["healthy"] = True
+        self._update(task, P.TASK_RUNNING, **extra)
+        if info.HasField("check"):
+            delay = (info.check.delay_seconds if timing.honor_check_delays else 0.0) + timing.check_exec_s
+            self._schedule(delay, self._lifecycle_ready, task, epoch)
+        if timing.finish_after_s is not None:
+            self._schedule(timing.finish_after_s, self._lifecycle_exit, task, epoch, timing.exit_state)
+
+    def _lifecycle_ready(self, task: _Task, epoch: int) -> None:
+        if task.epoch != epoch or task.status.state != P.TASK_RUNNING:
+            return
+        cs = P.CheckStatusInfo(type=task.info.check.type)
+        cs.command.exit_code = 0
+        extra = {"check_status": cs, "reason": P.TaskStatus.REASON_TASK_CHECK_STATUS_UPDATED}
+        if task.info.HasField("health_check"):
+            extra["healthy"] = True
+        self._update(task, P.TASK_RUNNING, **extra)
+
+    def _lifecycle_exit(self, task: _Task, epoch: int, state: int) -> None:
+        if task.epoch != epoch or task.status.state in TERMINAL:
+            return
+        self._update(task, state, message="task exited")
+
+    def _kill(self, fid: str, task_id: str) -> None:
+        t = self._find_task(task_id)
+        if t is None or t.framework_id != fid:
+            st = P.TaskStatus(state=P.TASK_LOST, source=P.TaskStatus.SOURCE_MASTER,
+                              reason=P.TaskStatus.REASON_RECONCILIATION, message="Attempted to kill an unknown task",
+                              timestamp=time.time())
+            st.task_id.value = task_id
+            fw = self._fw(fid)
+            if fw is not None:
+                fw.driver._deliver(lambda s, d=fw.driver: s.status_update(d, st))
+            return
+        if t.status.state in TERMINAL:
+            return
+        self._update(t, P.TASK_KILLED, message="Task killed by scheduler")
+
+    def _find_task(self, task_id: str) -> Optional[_Task]:
+        for a in self.agents.values():
+            t = a.tasks.get(task_id)
+            if t is not None:
+                return t
+        return None
+
+    def _update(self, task: _Task, state: int, deliver: bool = True, **fields) -> None:
+        st = P.TaskStatus(state=state, timestamp=time.time())
+        st.task_id.CopyFrom(task.info.task_id)
+        st.agent_id.value = task.agent_id
+        if task.executor_id:
+            st.executor_id.value = task.executor_id
+        st.source = fields.pop("source", P.TaskStatus.SOURCE_EXECUTOR)
+        cs = fields.pop("check_status", None)
+        if cs is not None:
+            st.check_status.CopyFrom(cs)
+        for k, v in fields.items():
+            setattr(st, k, v)
+        if task.gpu_devices:
+            st.labels.labels.add(key="gpu_devices", value=",".join(str(d) for d in task.gpu_devices))
+        st.container_status.network_infos.add().ip_addresses.add(ip_address="127.0.0.1")
+        st.uuid = uuid.uuid4().bytes
+        task.status = st
+        if state in TERMINAL:
+            task.epoch += 1
+            self._release_task(task)
+        fw = self.frameworks.get(task.framework_id)
+        for fn in self._listeners:
+            try:
+                fn(task.framework_id, st)
+            except Exception:  # noqa: BLE001
+                LOGGER.exception("status listener failed")
+        if deliver and fw is not None and fw.connected:
+            fw.driver._deliver(lambda s, d=fw.driver, st=st: s.status_update(d, st))
+
+    def _release_task(self, task: _Task) -> None:
+        a = self.agents.get(task.agent_id)
+        if a is None:
+            return
+        for r in task.resources:
+            a.available.add(r)
+        task.resources = []
+        a.free_gpus.extend(task.gpu_devices)
+        a.free_gpus.sort()
+        task.gpu_devices = []
+        key = (task.framework_id, task.executor_id)
+        e = a.executors.get(key)
+        if e is not None:
+            e.tasks.discard(task.info.task_id.value)
+            if not e.tasks:
+                for r in e.resources:
+                    a.available.add(r)
+                del a.executors[key]
+
+    def _deliver_synthetic(self, fid: str, t: P.TaskInfo, state: int, reason: int, message: str) -> None:
+        fw = self._fw(fid)
+        if fw is None:
+            return
+        st = P.TaskStatus(state=state, source=P.TaskStatus.SOURCE_MASTER, reason=reason, message=message,
+                          timestamp=time.time())
+        st.task_id.CopyFrom(t.task_id)
+        fw.driver._deliver(lambda s, d=fw.driver: s.status_update(d, st))
+
+    def _reconcile(self, fid: str, statuses: List[P.TaskStatus]) -> None:
+        fw = self._fw(fid)
+        if fw is None:
+            return
+        out = []
+        if not statuses:
+            for a in self.agents.values():
+                for t in a.tasks.values():
+                    if t.framework_id == fid and t.status.state not in TERMINAL:
+                        out.append(t.status)
+        else:
+            for s in statuses:
+                t = self._find_task(s.task_id.value)
+                if t is not None and t.framework_id == fid:
+                    c = P.TaskStatus()
+                    c.CopyFrom(t.status)
+                    c.reason = P.TaskStatus.REASON_RECONCILIATION
+                    out.append(c)
+                else:
+                    st = P.TaskStatus(state=P.TASK_LOST, source=P.TaskStatus.SOURCE_MASTER,
+                                      reason=P.TaskStatus.REASON_RECONCILIATION, message="Reconciliation: task unknown",
+                                      timestamp=time.time())
+                    st.task_id.CopyFrom(s.task_id)
+                    out.append(st)
+        for st in out:
+            fw.driver._deliver(lambda s, d=fw.driver, st=st: s.status_update(d, st))
+
+
+class LocalSchedulerDriver(SchedulerDriver):
+    """Driver bound to a ``LocalMaster``; callbacks go to a FrameworkScheduler-like sink."""
+
+    def __init__(self, master: LocalMaster, scheduler, framework_info: P.FrameworkInfo):
+        self.master = master
+        self.scheduler = scheduler
+        self.framework_info = framework_info
+        self._framework_id: Optional[str] = None
+        self._stopped = threading.Event()
+        self.acknowledged: List[bytes] = []
+
+    # deliveries run on the master thread, in order
+    def _deliver(self, fn) -> None:
+        if self._stopped.is_set():
+            return
+        try:
+            fn(self.scheduler)
+        except Exception:  # noqa: BLE001
+            LOGGER.exception("Scheduler callback failed")
+
+    @property
+    def framework_id(self) -> Optional[str]:
+        return self._framework_id
+
+    def start(self) -> None:
+        self.master.subscribe(self, self.framework_info)
+
+    def run(self) -> int:
+        self.start()
+        self._stopped.wait()
+        return 0
+
+    def join(self, timeout: Optional[float] = None) -> bool:
+        return self._stopped.wait(timeout)
+
+    def accept_offers(self, offer_ids, operations, filters=None) -> None:
+        refuse = filters.refuse_seconds if filters is not None else 5.0
+        self.master.accept(self._framework_id, [o.value for o in offer_ids], list(operations), refuse)
+
+    def decline_offer(self, offer_id, filters=None) -> None:
+        self.decline_offers([offer_id], filters)
+
+    def decline_offers(self, offer_ids, filters=None) -> None:
+        refuse = filters.refuse_seconds if filters is not None else 5.0
+        self.master.decline(self._framework_id, [o.value for o in offer_ids], refuse)
+
+    def kill_task(self, task_id) -> None:
+        self.master.kill(self._framework_id, task_id.value)
+
+    def reconcile_tasks(self, statuses) -> None:
+        self.master.reconcile(self._framework_id, list(statuses))
+
+    def revive_offers(self) -> None:
+        self.master.revive(self._framework_id)
+
+    def suppress_offers(self) -> None:
+        self.master.suppress(self._framework_id)
+
+    def acknowledge_status_update(self, status) -> None:
+        if status.uuid:
+            self.acknowledged.append(status.uuid)
+
+    def teardown(self) -> None:
+        if self._framework_id:
+            self.master.teardown(self._framework_id)
+
+    def stop(self, failover: bool = True) -> None:
+        if self._framework_id:
+            if failover:
+                self.master.disconnect(self._framework_id)
+            else:
+                self.master.teardown(self._framework_id)
+        self._stopped.set()
+
+
+def local_master_from_env(env) -> LocalMaster:
+    """An in-process cluster sized from ``SDK_LOCAL_*`` variables (``SDK_MESOS_MASTER=local``)."""
+    n = env.get_optional_int("SDK_LOCAL_AGENTS", 3)
+    gpus = env.get_optional_int("SDK_LOCAL_AGENT_GPUS", 0)
+    master = LocalMaster(allocation_interval_s=env.get_optional_double("SDK_LOCAL_ALLOCATION_INTERVAL_S", 1.0))
+    for i in range(n):
+        attrs = {"gpu_vendor": "amd", "gpu_model": "MI355X"} if gpus else {}
+        master.add_agent(AgentSpec(hostname=f"agent-{i}.local",
+                                   cpus=env.get_optional_double("SDK_LOCAL_AGENT_CPUS", 8.0),
+                                   mem=env.get_optional_double("SDK_LOCAL_AGENT_MEM", 32768.0),
+                                   disk=env.get_optional_double("SDK_LOCAL_AGENT_DISK", 65536.0),
+                                   gpus=gpus, attributes=attrs))
+    return master

@@ -196,6 +196,24 @@ class SchedulerConfig:
     def offer_wait_s(self) -> float:
         return self.env.get_optional_double("SDK_OFFER_WAIT_S", 5.0)
 
+    def is_event_driven(self) -> bool:
+        """Wake the offer loop on every status update (reference: poll only)."""
+        return self.env.get_optional_boolean("SDK_EVENT_DRIVEN", True)
+
+    def offer_hold_s(self) -> float:
+        """Hold unused offers this long while WORKING instead of declining them for 1 h
+        (0 = reference behaviour: long decline + rate-limited revive)."""
+        return self.env.get_optional_double("SDK_OFFER_HOLD_S", 10.0)
+
+    def revive_interval_s(self) -> float:
+        return self.env.get_optional_double("SDK_REVIVE_INTERVAL_S", 5.0)
+
+    def implicit_reconcile_delay_s(self) -> float:
+        return self.implicit_reconcile_delay_ms() / 1000.0
+
+    def implicit_reconcile_period_s(self) -> float:
+        return self.implicit_reconcile_period_ms() / 1000.0
+
     def build_info(self) -> Dict[str, str]:
         return {
             "PACKAGE_NAME": self.env.get_optional("PACKAGE_NAME", ""),
