@@ -1,0 +1,74 @@
+#!/usr/bin/env python3
+"""Headline benchmark: helloworld deploy-plan COMPLETE wall-clock + pod recovery MTTR.
+
+    python bench.py --gpus N --steps K --warmup W
+
+N GPUs = N MI355X agents (one per GPU, ``gpus: 1`` pods pinned 1:1, readiness = HIP device
+probe on the pod's GPU). A *step* is one full cycle on a fresh cluster and fresh state:
+deploy -> inject TASK_FAILED (restart MTTR) -> ``pod replace`` (replace MTTR) -> teardown.
+``value`` is the mean deploy-plan COMPLETE wall-clock over the K timed steps (seconds, lower is
+better); the MTTRs are reported alongside. Weak scaling: one pod per GPU.
+
+Under ``torchrun`` every rank owns the agent for its GPU (LOCAL_RANK) and rank 0 runs the
+master + scheduler; agents talk to the master over TCP (``parallel.agent_link``).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import logging
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+
+def parse_args(argv=None):
+    ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--profile", default="mi355x", choices=["mi355x", "reference"])
+    ap.add_argument("--allocation-interval", type=float, default=1.0,
+                    help="fake Mesos master allocation interval (Mesos default 1 s)")
+    ap.add_argument("--no-gpu-probe", action="store_true", help="synthetic readiness (no HIP probe)")
+    ap.add_argument("--verbose", action="store_true")
+    return ap.parse_args(argv)
+
+
+def main(argv=None) -> int:
+    args = parse_args(argv)
+    logging.basicConfig(level=logging.INFO if args.verbose else logging.ERROR,
+                        format="%(asctime)s %(name)s %(levelname)s %(message)s")
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+
+    import torch
+
+    use_gpu = torch.cuda.is_available() and not args.no_gpu_probe
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        backend = "nccl" if torch.cuda.is_available() else "gloo"
+        if torch.cuda.is_available():
+            torch.cuda.set_device(local_rank)
+        dist.init_process_group(backend=backend)
+
+    from dcos_commons_amd.benchmarks.runner import run_bench
+
+    result = run_bench(args, rank=rank, world=world, local_rank=local_rank, use_gpu=use_gpu, dist=dist)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if dist is not None:
+        dist.barrier()
+        dist.destroy_process_group()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,155 @@
+"""Deploy wall-clock + pod-recovery MTTR benchmark (the BASELINE.json headline metric).
+
+One *cycle* on a fresh cluster and fresh state:
+  1. start the helloworld scheduler and time until ``GET /v1/plans/deploy`` answers 200
+     (deploy plan COMPLETE: every pod RUNNING and, for GPU pods, its readiness check -- the HIP
+     device probe on the GPU it was given -- passed);
+  2. inject ``TASK_FAILED`` into pod ``hello-0`` and time until it is back (new task RUNNING +
+     ready) and the ``recovery`` plan is COMPLETE (MTTR, transient restart);
+  3. ``POST /v1/pod/hello-0/replace`` and time the same way (MTTR, permanent replace);
+  4. tear the scheduler down.
+
+Cluster: ``n_agents`` agents, each owning one MI355X (``gpus: 1``, ``HIP_VISIBLE_DEVICES``
+pinned by device index); helloworld ``gpu.yml`` with one pod per agent (``hostname:UNIQUE``).
+The ``reference`` profile replays the reference scheduler's timing constants on the same harness
+(5 s offer poll, long declines + 5 s-throttled revives, no event-driven wake-up).
+"""
+from __future__ import annotations
+
+import os
+import time
+from dataclasses import dataclass
+from typing import Callable, Dict, List, Optional
+
+from dcos_commons_amd.framework.process_exit import ProcessExit
+from dcos_commons_amd.mesos import protos as P
+from dcos_commons_amd.mesos.local_master import AgentSpec, LocalMaster, LocalSchedulerDriver, TaskBehavior, TaskTiming
+from dcos_commons_amd.offer.taskdata.labels import TaskLabelReader
+from dcos_commons_amd.scheduler.scheduler_builder import SchedulerBuilder
+from dcos_commons_amd.scheduler.scheduler_config import SchedulerConfig
+from dcos_commons_amd.scheduler.scheduler_runner import SchedulerRunner
+from dcos_commons_amd.specification.yaml.mappers import ServiceSpecGenerator
+from dcos_commons_amd.specification.yaml.raw import RawServiceSpec
+from dcos_commons_amd.storage.mem_persister import MemPersister
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+SPECS = os.path.join(ROOT, "frameworks", "helloworld", "specs")
+
+PROFILES = {
+    # this framework: event-driven offer loop, bounded offer holding
+    "mi355x": {},  # framework defaults: event-driven wake-ups, 10 s offer holding, 1 s revive spacing
+    # the reference's cadence on the same harness
+    "reference": {"SDK_EVENT_DRIVEN": "false", "SDK_OFFER_HOLD_S": "0", "SDK_OFFER_WAIT_S": "5",
+                  "SDK_REVIVE_INTERVAL_S": "5", "SDK_RESERVATION_GC_ALL_OFFERS": "false"},
+}
+
+
+@dataclass
+class CycleResult:
+    deploy_s: float
+    mttr_restart_s: float
+    mttr_replace_s: float
+    total_s: float
+
+
+def helloworld_env(n_pods: int, gpus_per_pod: int, probe_cmd: str) -> Dict[str, str]:
+    return {
+        "FRAMEWORK_NAME": "hello-world", "FRAMEWORK_PRINCIPAL": "hello-world-principal", "FRAMEWORK_USER": "nobody",
+        "HELLO_COUNT": str(n_pods), "HELLO_PLACEMENT": '[["hostname", "UNIQUE"]]', "HELLO_CPUS": "0.1",
+        "HELLO_GPUS": str(gpus_per_pod), "HELLO_MEM": "252", "HELLO_DISK": "25", "SLEEP_DURATION": "1000",
+        "GPU_PROBE_CMD": probe_cmd, "WORLD_COUNT": "0", "WORLD_PLACEMENT": "", "WORLD_CPUS": "0.2",
+        "WORLD_MEM": "512", "WORLD_DISK": "25", "WORLD_READINESS_CHECK_INTERVAL": "5",
+        "WORLD_READINESS_CHECK_DELAY": "0", "WORLD_READINESS_CHECK_TIMEOUT": "10",
+    }
+
+
+class DeployBench:
+    def __init__(self, n_agents: int, profile: str = "mi355x", spec_file: str = "gpu.yml",
+                 check_runner: Optional[Callable[[P.TaskInfo, List[int]], bool]] = None,
+                 gpu_devices: Optional[List[int]] = None, allocation_interval_s: float = 1.0,
+                 timeout_s: float = 120.0, agent_runners: Optional[List[Callable]] = None):
+        self.n = n_agents
+        self.profile = profile
+        self.spec_file = spec_file
+        self.check_runner = check_runner
+        self.gpu_devices = gpu_devices if gpu_devices is not None else list(range(n_agents))
+        self.allocation_interval_s = allocation_interval_s
+        self.timeout_s = timeout_s
+        self.agent_runners = agent_runners  # per-agent check runner (remote GPU agents)
+
+    # -- helpers ---------------------------------------------------------------------------
+    def _wait(self, pred, what: str) -> float:
+        t0 = time.perf_counter()
+        while True:
+            if pred():
+                return time.perf_counter() - t0
+            if time.perf_counter() - t0 > self.timeout_s:
+                raise TimeoutError(f"timed out after {self.timeout_s}s waiting for {what}")
+            time.sleep(0.001)
+
+    @staticmethod
+    def _pod_ready(state_store, task_name: str, old_task_id: Optional[str]) -> bool:
+        info = state_store.fetch_task(task_name)
+        st = state_store.fetch_status(task_name)
+        if info is None or st is None or st.state != P.TASK_RUNNING:
+            return False
+        if old_task_id is not None and st.task_id.value == old_task_id:
+            return False
+        if st.task_id.value != info.task_id.value:
+            return False
+        return TaskLabelReader(info).is_readiness_check_succeeded(st)
+
+    def _make_master(self) -> LocalMaster:
+        behavior = TaskBehavior(TaskTiming(), check_runner=self.check_runner)
+        master = LocalMaster(allocation_interval_s=self.allocation_interval_s, behavior=behavior)
+        for i in range(self.n):
+            dev = self.gpu_devices[i % len(self.gpu_devices)]
+            master.add_agent(AgentSpec(hostname=f"mi355x-agent-{i}", cpus=16, mem=65536, disk=100000, gpus=1,
+                                       gpu_devices=[dev],
+                                       attributes={"gpu_vendor": "amd", "gpu_model": "MI355X", "xgmi_hive": "0"}),
+                             check_runner=self.agent_runners[i] if self.agent_runners else None)
+        return master
+
+    # -- one cycle -------------------------------------------------------------------------
+    def run_cycle(self) -> CycleResult:
+        ProcessExit.set_test_mode(True)
+        t_cycle = time.perf_counter()
+        env = helloworld_env(self.n, 1, "amd-gpu-probe --readiness")
+        overrides = dict(PROFILES[self.profile])
+        overrides.update({"PORT_API": "0", "SDK_PERSISTER": "mem"})
+        cfg = SchedulerConfig.for_testing(**overrides)
+        path = os.path.join(SPECS, self.spec_file)
+        raw = RawServiceSpec.new_builder(path).set_env(env).build()
+        spec = ServiceSpecGenerator(raw, cfg, SPECS, env).build()
+        master = self._make_master()
+        builder = SchedulerBuilder(spec, cfg, MemPersister()).set_plans_from(raw)
+        runner = SchedulerRunner(builder, driver_factory=lambda s, info: LocalSchedulerDriver(master, s, info))
+        try:
+            t0 = time.perf_counter()
+            runner.run(block=False)
+            router = runner.framework_runner.api_server.router
+            state_store = runner.scheduler.state_store
+            self._wait(lambda: router.get("/v1/plans/deploy").status == 200, "deploy plan COMPLETE")
+            deploy_s = time.perf_counter() - t0
+
+            # transient restart MTTR
+            old = state_store.fetch_task("hello-0-server").task_id.value
+            t1 = time.perf_counter()
+            master.fail_task(old)
+            self._wait(lambda: self._pod_ready(state_store, "hello-0-server", old) and
+                       router.get("/v1/plans/recovery").status == 200, "restart recovery")
+            mttr_restart = time.perf_counter() - t1
+
+            # permanent replace MTTR
+            old = state_store.fetch_task("hello-0-server").task_id.value
+            t2 = time.perf_counter()
+            r = router.post("/v1/pod/hello-0/replace")
+            if r.status != 200:
+                raise RuntimeError(f"replace failed: {r.status} {r.payload()!r}")
+            self._wait(lambda: self._pod_ready(state_store, "hello-0-server", old) and
+                       router.get("/v1/plans/recovery").status == 200, "replace recovery")
+            mttr_replace = time.perf_counter() - t2
+        finally:
+            runner.stop()
+            master.shutdown()
+        return CycleResult(deploy_s, mttr_restart, mttr_replace, time.perf_counter() - t_cycle)

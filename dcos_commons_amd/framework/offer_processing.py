@@ -123,6 +123,18 @@ class TokenBucket:
                 return True
             return False
 
+    def seconds_until_available(self) -> float:
+        """How long until ``try_acquire`` can next succeed (0 if it can now)."""
+        with self._lock:
+            self._refill()
+            now = self.clock()
+            wait = 0.0
+            if self._last_acquire is not None:
+                wait = max(0.0, self.acquire_interval_s - (now - self._last_acquire))
+            if self.count <= 0:
+                wait = max(wait, self.increment_interval_s - (now - self._last_increment))
+            return wait
+
     def reset(self) -> None:
         with self._lock:
             self.count = self.initial
@@ -216,6 +228,30 @@ def to_cleanup_recommendations(offer_resources_list) -> list:
     return destroys + unreserves
 
 
+def _targeted_resource_ids(recs) -> set:
+    from dcos_commons_amd.offer.resources import get_resource_id
+
+    out = set()
+    for r in recs:
+        if isinstance(r, (DestroyOfferRecommendation, UnreserveOfferRecommendation)):
+            rid = get_resource_id(r.resource)
+            if rid is not None:
+                out.add(rid)
+    return out
+
+
+def _drop_targeted(offer_resources_list, targeted: set):
+    from dcos_commons_amd.offer.resources import get_resource_id
+    from dcos_commons_amd.scheduler.mesos_event_client import OfferResources
+
+    out = []
+    for orr in offer_resources_list:
+        keep = [r for r in orr.resources if get_resource_id(r) not in targeted]
+        if keep:
+            out.append(OfferResources(orr.offer, keep))
+    return out
+
+
 def decline(offers, refuse_seconds: float) -> None:
     d = driver.get_instance()
     f = P.Filters(refuse_seconds=refuse_seconds)
@@ -238,7 +274,7 @@ def decline_long(offers) -> None:
 class OfferProcessor:
     def __init__(self, client, persister, scheduler_config=None, token_bucket: Optional[TokenBucket] = None,
                  queue_capacity: int = DEFAULT_QUEUE_CAPACITY, offer_wait_s: Optional[float] = None,
-                 hold_s: float = 0.0, event_driven: bool = False):
+                 hold_s: float = 0.0, event_driven: bool = False, gc_all_offers: bool = False):
         self.client = client
         self.persister = persister
         self.offer_wait_s = offer_wait_s if offer_wait_s is not None else (
@@ -250,6 +286,11 @@ class OfferProcessor:
         self.multithreaded = True
         self.hold_s = hold_s
         self.event_driven = event_driven
+        # reference: stale reservations are only collected from offers nothing was launched on,
+        # and only while the service is WORKING (OfferProcessor.java:300-330), so a pod replaced
+        # onto the same agent, or a scheduler that goes idle, leaks them until the next work.
+        # gc_all_offers collects them from every offer, idle or not.
+        self.gc_all_offers = gc_all_offers
         self._held: Dict[str, tuple] = {}  # offer id -> (offer, hold deadline)
         self._initialized = False
         self._deregistered = False
@@ -284,7 +325,12 @@ class OfferProcessor:
     def _loop(self) -> None:
         while not self._stop.is_set():
             try:
-                self.process_queued_offers(self.offer_wait_s)
+                wait = self.offer_wait_s
+                if self.event_driven and self.revive_manager.revive_requested:
+                    # a throttled revive is retried the moment the bucket allows it, not at the
+                    # next offer poll
+                    wait = min(wait, max(0.001, self.revive_manager.bucket.seconds_until_available()))
+                self.process_queued_offers(wait)
             except Exception as e:  # noqa: BLE001
                 LOGGER.exception("Error encountered when processing offers, exiting to avoid zombie state")
                 ProcessExit.exit(ProcessExit.ERROR, e)
@@ -342,6 +388,8 @@ class OfferProcessor:
                     self._evaluate(offers, now)
                 elif offers:
                     self._held.clear()
+                    if self.gc_all_offers:
+                        offers = self._collect_garbage(offers)
                     decline_long(offers)
             self.revive_manager.revive_if_requested()
         finally:
@@ -368,15 +416,29 @@ class OfferProcessor:
                                "MultiServiceEventClient")
         return False
 
+    def _collect_garbage(self, offers):
+        """Idle path: release unexpected reservations, return the offers still unused."""
+        un = self.client.get_unexpected_resources(offers)
+        if un.result != UnexpectedResult.PROCESSED:
+            return offers
+        recs = to_cleanup_recommendations(un.offer_resources)
+        metrics.increment_recommendations(recs)
+        self.accepter.accept(recs)
+        return filter_out_accepted(offers, recs)
+
     def _evaluate(self, offers, now: float) -> None:
         resp = self.client.offers(offers)
         unused = filter_out_accepted(offers, resp.recommendations)
         cleanup_result = UnexpectedResult.PROCESSED
         cleanup_recs = []
-        if unused:
-            un = self.client.get_unexpected_resources(unused)
+        scan = offers if self.gc_all_offers else unused
+        if scan:
+            un = self.client.get_unexpected_resources(scan)
             cleanup_result = un.result
-            cleanup_recs = to_cleanup_recommendations(un.offer_resources)
+            found = un.offer_resources
+            if self.gc_all_offers:
+                found = _drop_targeted(found, _targeted_resource_ids(resp.recommendations))
+            cleanup_recs = to_cleanup_recommendations(found)
         unused = filter_out_accepted(unused, cleanup_recs)
         used = {o.id.value for o in offers} - {o.id.value for o in unused}
         for oid in used:

@@ -71,7 +71,7 @@ class _Handler(BaseHTTPRequestHandler):
 
 
 class ApiServer:
-    def __init__(self, port: int, resources: Iterable, host: str = "0.0.0.0"):
+    def __init__(self, port: int, resources: Iterable, host: str = "127.0.0.1"):
         self.router = Router(list(resources) + [MetricsResource()])
         handler = type("Handler", (_Handler,), {"router": self.router})
         self.httpd = ThreadingHTTPServer((host, port), handler)
@@ -82,7 +82,9 @@ class ApiServer:
     @staticmethod
     def start(scheduler_config, resources, started_callback: Callable[[], None], port: Optional[int] = None,
               scheduler_hostname: Optional[str] = None, wait_for_dns: bool = False) -> "ApiServer":
-        srv = ApiServer(scheduler_config.api_server_port() if port is None else port, resources)
+        # loopback unless the operator opts in to a wider bind (SDK_API_HOST)
+        host = scheduler_config.env.get_optional("SDK_API_HOST", "127.0.0.1")
+        srv = ApiServer(scheduler_config.api_server_port() if port is None else port, resources, host)
         timeout = scheduler_config.api_server_init_timeout_s()
 
         def run():

@@ -127,12 +127,29 @@ class TaskTiming:
 
 
 class TaskBehavior:
-    """Decides the synthetic lifecycle of a launched task; override ``timing`` for scenarios."""
+    """Decides the lifecycle of a launched task; override ``timing`` for scenarios.
+
+    ``check_runner(task_info, gpu_devices) -> bool`` executes a task's check (readiness) for real
+    (e.g. the HIP GPU probe on the task's devices) on a worker thread; without it checks pass
+    synthetically after ``delay_seconds + check_exec_s``.
+    """
 
     def __init__(self, default: Optional[TaskTiming] = None,
-                 overrides: Optional[Dict[str, TaskTiming]] = None):
+                 overrides: Optional[Dict[str, TaskTiming]] = None,
+                 check_runner: Optional[Callable[[P.TaskInfo, List[int]], bool]] = None,
+                 check_workers: int = 8):
         self.default = default or TaskTiming()
         self.overrides = dict(overrides or {})
+        self.check_runner = check_runner
+        self._pool = None
+        self._workers = check_workers
+
+    def pool(self):
+        if self._pool is None:
+            from concurrent.futures import ThreadPoolExecutor
+
+            self._pool = ThreadPoolExecutor(max_workers=self._workers, thread_name_prefix="task-check")
+        return self._pool
 
     def timing(self, task: P.TaskInfo) -> TaskTiming:
         for k, v in self.overrides.items():
@@ -171,6 +188,7 @@ class _Agent:
         devices = spec.gpu_devices if spec.gpu_devices is not None else list(range(spec.gpus))
         self.free_gpus: List[int] = list(devices)
         self.active = True
+        self.check_runner = None  # per-agent check executor (e.g. a remote GPU agent)
 
     def info_attributes(self) -> List[P.Attribute]:
         return [text_attribute(k, v) for k, v in sorted(self.spec.attributes.items())]
@@ -184,7 +202,9 @@ class _Framework:
     roles: Set[str]
     suppressed: bool = False
     connected: bool = True
-    filters: Dict[str, float] = field(default_factory=dict)  # agent id -> filter expiry
+    # agent id -> [(expiry, declined resources)]: Mesos' RefusedOfferFilter -- an agent's offer is
+    # filtered only while everything it would contain is within a declined set
+    filters: Dict[str, list] = field(default_factory=dict)
 
 
 @dataclass
@@ -267,10 +287,11 @@ class LocalMaster:
         self._listeners.append(fn)
 
     # -- cluster management --------------------------------------------------------------
-    def add_agent(self, spec: AgentSpec) -> str:
+    def add_agent(self, spec: AgentSpec, check_runner=None) -> str:
         def do():
             aid = f"agent-{len(self.agents)}-{uuid.uuid4().hex[:6]}"
             self.agents[aid] = _Agent(aid, spec)
+            self.agents[aid].check_runner = check_runner
             self._allocate()
             return aid
         return self.call(do)
@@ -439,14 +460,16 @@ class LocalMaster:
                     continue
                 if any(o.agent_id == a.id and o.framework_id == fw.id for o in self.offers.values()):
                     continue
-                exp = fw.filters.get(a.id)
-                if exp is not None:
-                    if exp > now:
-                        continue
-                    del fw.filters[a.id]
                 mine = [r for r in a.available.to_resources() if self._offerable(fw, r)]
                 if not mine:
                     continue
+                flist = [f for f in fw.filters.get(a.id, []) if f[0] > now]
+                if flist:
+                    fw.filters[a.id] = flist
+                    if any(all(f[1].contains(r) for r in mine) for f in flist):
+                        continue
+                else:
+                    fw.filters.pop(a.id, None)
                 for r in mine:
                     a.available.subtract(r)
                 alloc_role = sorted(fw.roles)[0]
@@ -498,8 +521,8 @@ class LocalMaster:
             r.ClearField("allocation_info")
             a.available.add(r)
         fw = self.frameworks.get(o.framework_id)
-        if fw is not None and refuse_s > 0:
-            fw.filters[o.agent_id] = max(fw.filters.get(o.agent_id, 0.0), self.clock() + refuse_s)
+        if fw is not None and refuse_s > 0 and rs:
+            fw.filters.setdefault(o.agent_id, []).append((self.clock() + refuse_s, ResourceBag(rs)))
 
     def _decline(self, fid: str, offer_ids: List[str], refuse_s: float) -> None:
         for oid in offer_ids:
@@ -661,9 +684,46 @@ class LocalMaster:
         self._update(task, P.TASK_RUNNING, **extra)
         if info.HasField("check"):
             delay = (info.check.delay_seconds if timing.honor_check_delays else 0.0) + timing.check_exec_s
-            self._schedule(delay, self._lifecycle_ready, task, epoch)
+            if self._check_runner(task) is not None:
+                self._schedule(delay, self._run_check, task, epoch)
+            else:
+                self._schedule(delay, self._lifecycle_ready, task, epoch)
         if timing.finish_after_s is not None:
             self._schedule(timing.finish_after_s, self._lifecycle_exit, task, epoch, timing.exit_state)
+
+    def _check_runner(self, task: _Task):
+        a = self.agents.get(task.agent_id)
+        if a is not None and a.check_runner is not None:
+            return a.check_runner
+        return self.behavior.check_runner
+
+    def _run_check(self, task: _Task, epoch: int) -> None:
+        if task.epoch != epoch or task.status.state != P.TASK_RUNNING:
+            return
+        runner = self._check_runner(task)
+        devices = list(task.gpu_devices)
+
+        def work():
+            try:
+                ok = bool(runner(task.info, devices))
+            except Exception:  # noqa: BLE001
+                LOGGER.exception("check of %s raised", task.info.name)
+                ok = False
+            self._schedule(0, self._check_result, task, epoch, ok)
+        self.behavior.pool().submit(work)
+
+    def _check_result(self, task: _Task, epoch: int, ok: bool) -> None:
+        if task.epoch != epoch or task.status.state != P.TASK_RUNNING:
+            return
+        if ok:
+            self._lifecycle_ready(task, epoch)
+            return
+        prev = task.status.check_status.command.exit_code if task.status.HasField("check_status") else None
+        if prev != 1:
+            cs = P.CheckStatusInfo(type=task.info.check.type)
+            cs.command.exit_code = 1
+            self._update(task, P.TASK_RUNNING, check_status=cs, reason=P.TaskStatus.REASON_TASK_CHECK_STATUS_UPDATED)
+        self._schedule(task.info.check.interval_seconds, self._run_check, task, epoch)
 
     def _lifecycle_ready(self, task: _Task, epoch: int) -> None:
         if task.epoch != epoch or task.status.state != P.TASK_RUNNING:

@@ -206,7 +206,15 @@ class SchedulerConfig:
         return self.env.get_optional_double("SDK_OFFER_HOLD_S", 10.0)
 
     def revive_interval_s(self) -> float:
-        return self.env.get_optional_double("SDK_REVIVE_INTERVAL_S", 5.0)
+        """Minimum spacing of REVIVE calls. The reference hard-codes 5 s (TokenBucket.java:18-24);
+        the 256-token budget (+1 per 256 s) still bounds the sustained rate, so a 1 s burst spacing
+        costs the master little and takes up to 4 s off every recovery that needs a revive."""
+        return self.env.get_optional_double("SDK_REVIVE_INTERVAL_S", 1.0)
+
+    def is_reservation_gc_on_all_offers(self) -> bool:
+        """Release stale reservations from every offer, idle or not (reference: unused offers
+        while WORKING only)."""
+        return self.env.get_optional_boolean("SDK_RESERVATION_GC_ALL_OFFERS", True)
 
     def implicit_reconcile_delay_s(self) -> float:
         return self.implicit_reconcile_delay_ms() / 1000.0

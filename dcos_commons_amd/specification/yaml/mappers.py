@@ -59,6 +59,15 @@ class ConfigTemplateReader:
             return f.read()
 
 
+def _text(v):
+    """Jackson coerces YAML scalars bound to String fields (``cmd: true`` -> "true")."""
+    if v is None or isinstance(v, str):
+        return v
+    if isinstance(v, bool):
+        return "true" if v else "false"
+    return str(v)
+
+
 def _labels(csv: str) -> Dict[str, str]:
     out = {}
     for kv in csv.split(","):
@@ -218,20 +227,20 @@ def _convert_task(rt, reader: ConfigTemplateReader, task_name, additional_env, r
                   pre_reserved_role, principal, network_names) -> TaskSpec:
     env = rt.get("env") or {}
     env = {str(k): ("" if v is None else (str(v).lower() if isinstance(v, bool) else str(v))) for k, v in env.items()}
-    command = CommandSpec.build(rt.get("cmd"), env, additional_env) if rt.get("cmd") is not None else None
+    command = CommandSpec.build(_text(rt.get("cmd")), env, additional_env) if rt.get("cmd") is not None else None
     configs = []
     for cname, c in (rt.get("configs") or {}).items():
         configs.append(ConfigFileSpec(cname, c.get("dest"), reader.read(c.get("template"))))
     health = None
     if rt.get("health-check") is not None:
         h = rt["health-check"]
-        health = HealthCheckSpec(h.get("cmd"), h.get("max-consecutive-failures"), h.get("delay"),
+        health = HealthCheckSpec(_text(h.get("cmd")), h.get("max-consecutive-failures"), h.get("delay"),
                                  h.get("interval"), h.get("timeout"), h.get("grace-period"))
         health.validate()
     readiness = None
     if rt.get("readiness-check") is not None:
         r = rt["readiness-check"]
-        readiness = ReadinessCheckSpec(r.get("cmd"), r.get("interval"), r.get("timeout"),
+        readiness = ReadinessCheckSpec(_text(r.get("cmd")), r.get("interval"), r.get("timeout"),
                                        r.get("delay") if r.get("delay") is not None else 0)
         readiness.validate()
     discovery = None

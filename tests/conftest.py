@@ -1,0 +1,29 @@
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+REFERENCE = "/root/reference"
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (runs on the GPU box)")
+    config.addinivalue_line("markers", "slow: long-running")
+
+
+@pytest.fixture(autouse=True)
+def _test_mode():
+    """ProcessExit raises instead of exiting; deadlock detection raises instead of exiting."""
+    from dcos_commons_amd.framework.process_exit import ProcessExit
+
+    ProcessExit.set_test_mode(True)
+    yield
+
+
+def reference_path(*parts):
+    p = os.path.join(REFERENCE, *parts)
+    return p if os.path.exists(p) else None
