@@ -40,7 +40,8 @@ PROFILES = {
     "mi355x": {},  # framework defaults: event-driven wake-ups, 10 s offer holding, 1 s revive spacing
     # the reference's cadence on the same harness
     "reference": {"SDK_EVENT_DRIVEN": "false", "SDK_OFFER_HOLD_S": "0", "SDK_OFFER_WAIT_S": "5",
-                  "SDK_REVIVE_INTERVAL_S": "5", "SDK_RESERVATION_GC_ALL_OFFERS": "false"},
+                  "SDK_REVIVE_INTERVAL_S": "5", "SDK_RESERVATION_GC_ALL_OFFERS": "false",
+                  "SDK_FAST_UNSUPPRESS": "false"},
 }
 
 
@@ -132,6 +133,11 @@ class DeployBench:
             self._wait(lambda: router.get("/v1/plans/deploy").status == 200, "deploy plan COMPLETE")
             deploy_s = time.perf_counter() - t0
 
+            # failures are injected in steady state: deploy finished and the offer loop has gone
+            # idle (suppressed), as for a pod that fails long after its service deployed
+            rm = runner.framework_runner.framework_scheduler.offer_processor.revive_manager
+            self._wait(lambda: rm.is_suppressed, "scheduler idle after deploy")
+
             # transient restart MTTR
             old = state_store.fetch_task("hello-0-server").task_id.value
             t1 = time.perf_counter()
@@ -139,6 +145,8 @@ class DeployBench:
             self._wait(lambda: self._pod_ready(state_store, "hello-0-server", old) and
                        router.get("/v1/plans/recovery").status == 200, "restart recovery")
             mttr_restart = time.perf_counter() - t1
+
+            self._wait(lambda: rm.is_suppressed, "scheduler idle after restart")
 
             # permanent replace MTTR
             old = state_store.fetch_task("hello-0-server").task_id.value

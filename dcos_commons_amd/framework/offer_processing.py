@@ -57,10 +57,14 @@ class OfferQueue:
 
     def take_all(self, wait_s: float, wake: Optional[threading.Event] = None) -> List[P.Offer]:
         with self._cond:
+            if wake is not None and wake.is_set():
+                wake.clear()  # a kick that arrived while the last cycle ran is consumed here
+                wait_s = 0
             if not self._q and wait_s > 0:
                 deadline = time.monotonic() + wait_s
                 while not self._q:
                     if wake is not None and wake.is_set():
+                        wake.clear()
                         break
                     remaining = deadline - time.monotonic()
                     if remaining <= 0:
@@ -113,11 +117,12 @@ class TokenBucket:
             self.count = min(self.capacity, self.count + n)
             self._last_increment += n * self.increment_interval_s
 
-    def try_acquire(self) -> bool:
+    def try_acquire(self, ignore_spacing: bool = False) -> bool:
         with self._lock:
             self._refill()
             now = self.clock()
-            if self.count > 0 and (self._last_acquire is None or now - self._last_acquire >= self.acquire_interval_s):
+            if self.count > 0 and (ignore_spacing or self._last_acquire is None or
+                                   now - self._last_acquire >= self.acquire_interval_s):
                 self.count -= 1
                 self._last_acquire = now
                 return True
@@ -142,11 +147,21 @@ class TokenBucket:
 
 
 class ReviveManager:
-    def __init__(self, token_bucket: TokenBucket, suppress_enabled: bool = True):
+    """Revive/suppress bookkeeping (ReviveManager.java:40-150).
+
+    ``fast_unsuppress``: the first REVIVE after a SUPPRESS is not held to the burst spacing (it
+    still spends a token, so the 256-token budget bounds crash loops); spacing applies between
+    revives of one working period, where revive storms happen. The reference always waits for
+    the spacing, which puts up to 5 s on the MTTR of a failure that follows a recent revive.
+    """
+
+    def __init__(self, token_bucket: TokenBucket, suppress_enabled: bool = True, fast_unsuppress: bool = False):
         self.bucket = token_bucket
         self.suppress_enabled = suppress_enabled
+        self.fast_unsuppress = fast_unsuppress
         self.revive_requested = False
         self.is_suppressed = False
+        self._revive_bypass = False
 
     def notify_offers_received(self) -> None:
         self.is_suppressed = False
@@ -167,18 +182,22 @@ class ReviveManager:
             self.request_revive()
 
     def request_revive(self) -> None:
+        if self.is_suppressed and self.fast_unsuppress:
+            self._revive_bypass = True
         self.revive_requested = True
 
     def revive_if_requested(self) -> None:
         if not self.revive_requested:
             return
-        if not self.bucket.try_acquire():
+        if not self.bucket.try_acquire(ignore_spacing=self._revive_bypass):
             metrics.increment_revive_throttles()
             return
         d = driver.get_instance()
         if d is not None:
             d.revive_offers()
         self.revive_requested = False
+        self._revive_bypass = False
+        self.is_suppressed = False
         metrics.increment_revives()
 
 
@@ -228,6 +247,38 @@ def to_cleanup_recommendations(offer_resources_list) -> list:
     return destroys + unreserves
 
 
+def recycled_offers(offers, offer_resources_list):
+    """Copies of ``offers`` in which every stale reservation is shown as what its UNRESERVE
+    (after DESTROY) yields: the resource with its last reservation popped and no volume."""
+    from dcos_commons_amd.mesos.resource_math import pop_reservation, strip_volume
+
+    stale = {}
+    for orr in offer_resources_list:
+        stale.setdefault(orr.offer.id.value, []).extend(orr.resources)
+    out = []
+    for o in offers:
+        rs = stale.get(o.id.value)
+        if not rs:
+            out.append(o)
+            continue
+        c = P.Offer()
+        c.CopyFrom(o)
+        del c.resources[:]
+        remaining = list(rs)
+        for r in o.resources:
+            match = next((i for i, x in enumerate(remaining) if x == r), None)
+            if match is None:
+                c.resources.add().CopyFrom(r)
+                continue
+            remaining.pop(match)
+            freed = strip_volume(pop_reservation(r))
+            if r.HasField("allocation_info"):
+                freed.allocation_info.CopyFrom(r.allocation_info)
+            c.resources.add().CopyFrom(freed)
+        out.append(c)
+    return out
+
+
 def _targeted_resource_ids(recs) -> set:
     from dcos_commons_amd.offer.resources import get_resource_id
 
@@ -274,13 +325,14 @@ def decline_long(offers) -> None:
 class OfferProcessor:
     def __init__(self, client, persister, scheduler_config=None, token_bucket: Optional[TokenBucket] = None,
                  queue_capacity: int = DEFAULT_QUEUE_CAPACITY, offer_wait_s: Optional[float] = None,
-                 hold_s: float = 0.0, event_driven: bool = False, gc_all_offers: bool = False):
+                 hold_s: float = 0.0, event_driven: bool = False, gc_all_offers: bool = False,
+                 fast_unsuppress: bool = False):
         self.client = client
         self.persister = persister
         self.offer_wait_s = offer_wait_s if offer_wait_s is not None else (
             scheduler_config.offer_wait_s() if scheduler_config is not None else DEFAULT_OFFER_WAIT_S)
         suppress = scheduler_config.is_suppress_enabled() if scheduler_config is not None else True
-        self.revive_manager = ReviveManager(token_bucket or TokenBucket(), suppress)
+        self.revive_manager = ReviveManager(token_bucket or TokenBucket(), suppress, fast_unsuppress)
         self.queue = OfferQueue(queue_capacity)
         self.accepter = OfferAccepter()
         self.multithreaded = True
@@ -368,7 +420,6 @@ class OfferProcessor:
         raise TimeoutError("Timed out waiting for offers to be processed")
 
     def process_queued_offers(self, wait_s: float) -> None:
-        self._wake.clear()
         new_offers = self.queue.take_all(wait_s, self._wake if self.event_driven else None)
         if self._stop.is_set():
             return
@@ -427,19 +478,28 @@ class OfferProcessor:
         return filter_out_accepted(offers, recs)
 
     def _evaluate(self, offers, now: float) -> None:
-        resp = self.client.offers(offers)
-        unused = filter_out_accepted(offers, resp.recommendations)
+        pre_cleanup = []
         cleanup_result = UnexpectedResult.PROCESSED
-        cleanup_recs = []
-        scan = offers if self.gc_all_offers else unused
-        if scan:
-            un = self.client.get_unexpected_resources(scan)
+        eval_offers = offers
+        if self.gc_all_offers and offers:
+            # Reservation recycling: stale reservations are released at the head of the same
+            # ACCEPT that may re-reserve them (Mesos applies an ACCEPT's operations in order), so
+            # a replaced pod can land on the resources of its predecessor without waiting for
+            # another offer round (reference: UNRESERVE in one cycle, re-offer after the 1 s
+            # accept filter and the next allocation, OfferProcessor.java:300-330).
+            un = self.client.get_unexpected_resources(offers)
             cleanup_result = un.result
-            found = un.offer_resources
-            if self.gc_all_offers:
-                found = _drop_targeted(found, _targeted_resource_ids(resp.recommendations))
-            cleanup_recs = to_cleanup_recommendations(found)
-        unused = filter_out_accepted(unused, cleanup_recs)
+            if un.result == UnexpectedResult.PROCESSED and un.offer_resources:
+                pre_cleanup = to_cleanup_recommendations(un.offer_resources)
+                eval_offers = recycled_offers(offers, un.offer_resources)
+        resp = self.client.offers(eval_offers)
+        cleanup_recs = []
+        unused = filter_out_accepted(offers, list(resp.recommendations) + pre_cleanup)
+        if not self.gc_all_offers and unused:
+            un = self.client.get_unexpected_resources(unused)
+            cleanup_result = un.result
+            cleanup_recs = to_cleanup_recommendations(un.offer_resources)
+            unused = filter_out_accepted(unused, cleanup_recs)
         used = {o.id.value for o in offers} - {o.id.value for o in unused}
         for oid in used:
             self._held.pop(oid, None)
@@ -462,7 +522,7 @@ class OfferProcessor:
                 for o in unused:
                     self._held.pop(o.id.value, None)
                 decline_short(unused)
-        all_recs = list(resp.recommendations) + cleanup_recs
+        all_recs = pre_cleanup + list(resp.recommendations) + cleanup_recs
         metrics.increment_recommendations(all_recs)
         self.accepter.accept(all_recs)
 

@@ -458,8 +458,6 @@ class LocalMaster:
             for a in self.agents.values():
                 if not a.active:
                     continue
-                if any(o.agent_id == a.id and o.framework_id == fw.id for o in self.offers.values()):
-                    continue
                 mine = [r for r in a.available.to_resources() if self._offerable(fw, r)]
                 if not mine:
                     continue

@@ -216,6 +216,10 @@ class SchedulerConfig:
         while WORKING only)."""
         return self.env.get_optional_boolean("SDK_RESERVATION_GC_ALL_OFFERS", True)
 
+    def is_fast_unsuppress(self) -> bool:
+        """First REVIVE after a SUPPRESS skips the burst spacing (reference: never)."""
+        return self.env.get_optional_boolean("SDK_FAST_UNSUPPRESS", True)
+
     def implicit_reconcile_delay_s(self) -> float:
         return self.implicit_reconcile_delay_ms() / 1000.0
 
