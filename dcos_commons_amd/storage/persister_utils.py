@@ -16,8 +16,13 @@ LOGGER = logging.getLogger(__name__)
 
 
 def with_escaped_slashes(name: str) -> str:
-    """``/path/to/svc`` -> ``path__to__svc`` (reference SchedulerUtils.withEscapedSlashes)."""
-    return name.lstrip("/").replace("/", "__")
+    """``/path/to/svc`` -> ``path__to__svc`` (reference SchedulerUtils.withEscapedSlashes:
+    one leading slash dropped; names that already contain ``__`` are rejected)."""
+    if "__" in name:
+        raise ValueError(f"Service names may not contain double underscores: {name}")
+    if name.startswith(PATH_DELIM):
+        name = name[len(PATH_DELIM):]
+    return name.replace(PATH_DELIM, "__")
 
 
 def join_paths(*paths: str) -> str:
@@ -40,11 +45,17 @@ def get_path_elements(path: str) -> List[str]:
 
 
 def get_parent_paths(path: str) -> List[str]:
-    """All ancestor paths of ``path`` (not including itself), shallowest first."""
-    elems = get_path_elements(path)
-    out = []
-    for i in range(1, len(elems)):
-        out.append(PATH_DELIM.join(elems[:i]))
+    """All ancestor paths of ``path`` (not itself), shallowest first; a leading slash is kept
+    (PersisterUtils.getParentPaths: ``/a/b/c`` -> ``[/a, /a/b]``)."""
+    elements = path.split(PATH_DELIM)
+    out, cur = [], ""
+    for i in range(len(elements) - 1):
+        if not elements[i]:
+            continue
+        if i != 0:
+            cur += PATH_DELIM
+        cur += elements[i]
+        out.append(cur)
     return out
 
 
