@@ -59,6 +59,13 @@ class ConfigTemplateReader:
             return f.read()
 
 
+def _seccomp_unconfined(raw_pod) -> bool:
+    unconfined = bool(raw_pod.get("seccomp-unconfined"))
+    if unconfined and raw_pod.get("seccomp-profile-name"):
+        raise ValueError("seccomp-unconfined and seccomp-profile-name cannot both be set for a pod")
+    return unconfined
+
+
 def _text(v):
     """Jackson coerces YAML scalars bound to String fields (``cmd: true`` -> "true")."""
     if v is None or isinstance(v, str):
@@ -134,7 +141,9 @@ def _convert_ports(role, pre_reserved_role, principal, raw_ports, network_names)
                       principal=principal, pre_reserved_role=pre_reserved_role or ANY_ROLE,
                       env_key=rp.get("env-key"), port_name=name, visibility=visibility,
                       network_names=tuple(network_names))
-        ranges = tuple(RangeSpec(int(r["begin"]), int(r["end"])) for r in rp.get("ranges") or ())
+        # RangeSpec: a missing begin is MIN_PORT (0); a missing or zero end is MAX_PORT (65535)
+        ranges = tuple(RangeSpec(int(r["begin"]) if r.get("begin") is not None else 0,
+                                 int(r["end"]) if r.get("end") else 65535) for r in rp.get("ranges") or ())
         vip = rp.get("vip")
         if vip is None:
             spec = PortSpec(ranges=ranges, **common)
@@ -340,7 +349,7 @@ def convert_pod(raw_pod, reader: ConfigTemplateReader, pod_name: str, additional
         placement_rule=None if isinstance(rule, PassthroughRule) else rule, volumes=tuple(volumes),
         pre_reserved_role=pre_reserved_role, secrets=tuple(secrets),
         share_pid_namespace=bool(raw_pod.get("share-pid-namespace")), host_volumes=tuple(host_volumes),
-        seccomp_unconfined=bool(raw_pod.get("seccomp-unconfined")),
+        seccomp_unconfined=_seccomp_unconfined(raw_pod),
         seccomp_profile_name=raw_pod.get("seccomp-profile-name"),
         shared_memory=IpcMode.parse(raw_pod.get("ipc-mode")), shared_memory_size=raw_pod.get("shm-size"))
     pod.validate()

@@ -38,7 +38,7 @@ class MissingValue:
     __repr__ = __str__
 
 
-_ESCAPES = {"&": "&amp;", "<": "&lt;", ">": "&gt;", '"': "&quot;", "'": "&#39;", "`": "&#96;", "=": "&#61;"}
+_ESCAPES = {"&": "&amp;", "<": "&lt;", ">": "&gt;", '"': "&quot;", "'": "&#39;", "`": "&#x60;", "=": "&#x3D;"}
 _ESC_RE = re.compile(r"[&<>\"'`=]")
 
 
