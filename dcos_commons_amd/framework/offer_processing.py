@@ -250,7 +250,7 @@ def to_cleanup_recommendations(offer_resources_list) -> list:
 def recycled_offers(offers, offer_resources_list):
     """Copies of ``offers`` in which every stale reservation is shown as what its UNRESERVE
     (after DESTROY) yields: the resource with its last reservation popped and no volume."""
-    from dcos_commons_amd.mesos.resource_math import pop_reservation, strip_volume
+    from dcos_commons_amd.mesos.resource_math import ResourceBag, pop_reservation, strip_volume
 
     stale = {}
     for orr in offer_resources_list:
@@ -265,16 +265,20 @@ def recycled_offers(offers, offer_resources_list):
         c.CopyFrom(o)
         del c.resources[:]
         remaining = list(rs)
+        alloc = None
+        bag = ResourceBag()
         for r in o.resources:
+            if r.HasField("allocation_info") and alloc is None:
+                alloc = r.allocation_info
             match = next((i for i, x in enumerate(remaining) if x == r), None)
-            if match is None:
-                c.resources.add().CopyFrom(r)
-                continue
-            remaining.pop(match)
-            freed = strip_volume(pop_reservation(r))
-            if r.HasField("allocation_info"):
-                freed.allocation_info.CopyFrom(r.allocation_info)
-            c.resources.add().CopyFrom(freed)
+            bag.add(r if match is None else strip_volume(pop_reservation(r)))
+            if match is not None:
+                remaining.pop(match)
+        # Mesos merges identical resources (e.g. the freed cpus and the offer's unreserved cpus)
+        for r in bag.to_resources():
+            if alloc is not None:
+                r.allocation_info.CopyFrom(alloc)
+            c.resources.add().CopyFrom(r)
         out.append(c)
     return out
 

@@ -14,7 +14,7 @@ from typing import Dict, Iterable, List, Tuple, Union
 from dcos_commons_amd.mesos import protos as P
 from dcos_commons_amd.offer.values import _normalize, subtract_intervals
 
-EPS = 1e-6
+EPS = 5e-4  # Mesos scalars are fixed-point with 3 decimal digits
 Quantity = Union[float, List[Tuple[int, int]]]
 
 
@@ -69,7 +69,7 @@ class ResourceBag:
         if cur is None:
             self._q[k] = q
         elif isinstance(q, float):
-            self._q[k] = cur + q
+            self._q[k] = round((cur + q) * 1000.0) / 1000.0
         else:
             self._q[k] = _normalize(list(cur) + list(q))
 
@@ -94,7 +94,7 @@ class ResourceBag:
         if cur is None or not self.contains(r):
             raise InsufficientResources(f"{r.name} {q} not available (have {cur})")
         if isinstance(q, float):
-            nv = cur - q
+            nv = round((cur - q) * 1000.0) / 1000.0
         else:
             nv = subtract_intervals(cur, q)
         if _is_empty(nv):
@@ -115,7 +115,7 @@ class ResourceBag:
             r = P.Resource()
             r.CopyFrom(self._proto[k])
             if isinstance(q, float):
-                r.scalar.value = round(q, 6)
+                r.scalar.value = round(q, 3)
             else:
                 for b, e in q:
                     r.ranges.range.add(begin=b, end=e)

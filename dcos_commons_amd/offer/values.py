@@ -85,6 +85,12 @@ def get_zero(t: int) -> P.Value:
     raise ValueError(f"Unsupported type {t} for zero value")
 
 
+def fixed(x: float) -> float:
+    """Mesos scalar precision: values are fixed-point with three decimal digits, so 0.3 - 0.1 is
+    0.2 (not 0.19999999999999998) and a merged 0.1 + 0.2 cpus still fits a 0.2 request."""
+    return round(x * 1000.0) / 1000.0
+
+
 def _check_types(a: P.Value, b: P.Value, op: str) -> None:
     if a.type != b.type:
         raise ValueError(f"Values to {op} do not have matching type: {a.type} vs {b.type}")
@@ -94,7 +100,7 @@ def add(a: P.Value, b: P.Value) -> P.Value:
     _check_types(a, b, "add")
     if a.type == P.Value.SCALAR:
         v = P.Value(type=a.type)
-        v.scalar.value = a.scalar.value + b.scalar.value
+        v.scalar.value = fixed(a.scalar.value + b.scalar.value)
         return v
     if a.type == P.Value.RANGES:
         return intervals_to_value(merge_intervals(ranges_to_intervals(a.ranges.range),
@@ -106,7 +112,7 @@ def subtract(a: P.Value, b: P.Value) -> P.Value:
     _check_types(a, b, "subtract")
     if a.type == P.Value.SCALAR:
         v = P.Value(type=a.type)
-        v.scalar.value = a.scalar.value - b.scalar.value
+        v.scalar.value = fixed(a.scalar.value - b.scalar.value)
         return v
     if a.type == P.Value.RANGES:
         return intervals_to_value(subtract_intervals(ranges_to_intervals(a.ranges.range),
@@ -117,7 +123,7 @@ def subtract(a: P.Value, b: P.Value) -> P.Value:
 def compare(a: P.Value, b: P.Value) -> int:
     _check_types(a, b, "compare")
     if a.type == P.Value.SCALAR:
-        x, y = a.scalar.value, b.scalar.value
+        x, y = fixed(a.scalar.value), fixed(b.scalar.value)
         return -1 if x < y else (1 if x > y else 0)
     if a.type == P.Value.RANGES:
         ia = _normalize(ranges_to_intervals(a.ranges.range))
