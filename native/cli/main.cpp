@@ -1,0 +1,286 @@
+// sdk-cli: operator CLI for a running scheduler.
+//
+// Reference: cli/commands.go:39-52 and cli/commands/{plan,pod,endpoints,debug,update}.go with the
+// tree renderers of cli/queries/{plan,pod}.go. Talks to the scheduler's REST API directly over
+// HTTP/1.1 (no DC/OS cluster configuration needed): --url (or SDK_SCHEDULER_URL) is the scheduler
+// base URL; --service selects a service of a multi-service scheduler (/v1/service/<name>/...).
+#include <cstdlib>
+#include <iostream>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "../common/http.hpp"
+#include "../common/json.hpp"
+
+namespace {
+
+struct Ctx {
+  sdk::Url base;
+  std::string service;
+  bool json = false;
+  std::map<std::string, std::string> headers;
+};
+
+const char* kUnknown = "<UNKNOWN>";
+
+[[noreturn]] void die(const std::string& msg, int code = 1) {
+  std::cerr << msg << std::endl;
+  std::exit(code);
+}
+
+std::string api(const Ctx& c, const std::string& rest) {
+  return (c.service.empty() ? std::string("/v1") : "/v1/service/" + sdk::url_encode(c.service)) + rest;
+}
+
+sdk::HttpResponse call(const Ctx& c, const std::string& method, const std::string& path, const std::string& body = "",
+                       const std::string& content_type = "application/json") {
+  auto headers = c.headers;
+  if (!body.empty()) headers["Content-Type"] = content_type;
+  try {
+    return sdk::http_request(method, c.base, api(c, path), body, headers);
+  } catch (const std::exception& e) {
+    die(std::string("Failed to reach the scheduler: ") + e.what());
+  }
+}
+
+// prints the body; 2xx (and 208 "already reported") succeed, anything else is an error
+int emit(const sdk::HttpResponse& r, bool pretty_json = true) {
+  bool ok = (r.status >= 200 && r.status < 300);
+  std::string out = r.body;
+  if (pretty_json && !out.empty()) {
+    try {
+      out = sdk::Json::parse(out).dump(2);
+    } catch (...) {
+    }
+  }
+  if (!ok) {
+    std::cerr << "HTTP " << r.status << (out.empty() ? "" : ": " + out) << std::endl;
+    return r.status == 404 ? 2 : 1;
+  }
+  if (!out.empty()) std::cout << out << std::endl;
+  return 0;
+}
+
+std::string or_unknown(const sdk::Json& j) { return j.is_string() && !j.str().empty() ? j.str() : kUnknown; }
+
+std::string plan_tree(const std::string& name, const sdk::Json& plan) {
+  std::string out = name + " (" + or_unknown(plan["strategy"]) + " strategy) (" + or_unknown(plan["status"]) + ")\n";
+  const auto& phases = plan["phases"].arr();
+  for (size_t i = 0; i < phases.size(); ++i) {
+    bool last = i + 1 == phases.size();
+    const auto& ph = phases[i];
+    out += std::string(last ? "└─ " : "├─ ") + or_unknown(ph["name"]) + " (" + or_unknown(ph["strategy"]) +
+           " strategy) (" + or_unknown(ph["status"]) + ")\n";
+    const auto& steps = ph["steps"].arr();
+    for (size_t k = 0; k < steps.size(); ++k) {
+      out += std::string(last ? "   " : "│  ") + (k + 1 == steps.size() ? "└─ " : "├─ ") + or_unknown(steps[k]["name"]) +
+             " (" + or_unknown(steps[k]["status"]) + ")\n";
+    }
+  }
+  const auto& errors = plan["errors"].arr();
+  if (!errors.empty()) {
+    out += "\nErrors:\n";
+    for (const auto& e : errors) out += "- " + e.as_text() + "\n";
+  }
+  while (!out.empty() && out.back() == '\n') out.pop_back();
+  return out;
+}
+
+void append_tasks(std::string& out, const sdk::Json& tasks, const std::string& prefix) {
+  const auto& ts = tasks.arr();
+  for (size_t i = 0; i < ts.size(); ++i)
+    out += prefix + (i + 1 == ts.size() ? "└─ " : "├─ ") + or_unknown(ts[i]["name"]) + " (" +
+           or_unknown(ts[i]["status"]) + ")\n";
+}
+
+std::string pods_tree(const sdk::Json& j) {
+  std::string out = or_unknown(j["service"]) + "\n";
+  const auto& pods = j["pods"].arr();
+  for (size_t p = 0; p < pods.size(); ++p) {
+    bool lastp = p + 1 == pods.size();
+    out += std::string(lastp ? "└─ " : "├─ ") + or_unknown(pods[p]["name"]) + "\n";
+    std::string cp = lastp ? "   " : "│  ";
+    const auto& inst = pods[p]["instances"].arr();
+    for (size_t i = 0; i < inst.size(); ++i) {
+      bool lasti = i + 1 == inst.size();
+      out += cp + (lasti ? "└─ " : "├─ ") + or_unknown(inst[i]["name"]) + "\n";
+      append_tasks(out, inst[i]["tasks"], cp + (lasti ? "   " : "│  "));
+    }
+  }
+  while (!out.empty() && out.back() == '\n') out.pop_back();
+  return out;
+}
+
+std::string query(const std::vector<std::pair<std::string, std::string>>& kv) {
+  std::string q;
+  for (const auto& p : kv) {
+    if (p.second.empty()) continue;
+    q += (q.empty() ? "?" : "&") + p.first + "=" + sdk::url_encode(p.second);
+  }
+  return q;
+}
+
+std::string arg(const std::vector<std::string>& a, size_t i, const std::string& dflt = "") {
+  return i < a.size() ? a[i] : dflt;
+}
+
+void usage() {
+  std::cout <<
+      "usage: sdk-cli [--url URL] [--service NAME] [--json] <section> <command> [args]\n\n"
+      "  plan list | status [PLAN] | start PLAN [-p K=V]... | stop PLAN | pause PLAN [PHASE]\n"
+      "       resume PLAN [PHASE] | force-restart PLAN [PHASE [STEP]] | force-complete PLAN [PHASE [STEP]]\n"
+      "  pod  list | status [POD] | info POD | restart POD | replace POD | pause POD [-t TASK]... | resume POD [-t TASK]...\n"
+      "  endpoints [NAME]\n"
+      "  debug config list|show ID|target|target_id\n"
+      "  debug state framework_id|properties|property NAME|refresh_cache\n"
+      "  debug pod pause|resume POD [-t TASK]...\n"
+      "  describe | update status | health | metrics\n";
+}
+
+int plan_cmd(Ctx& c, const std::vector<std::string>& a) {
+  std::string cmd = arg(a, 0);
+  if (cmd == "list") return emit(call(c, "GET", "/plans"));
+  if (cmd == "status") {
+    std::string plan = arg(a, 1, "deploy");
+    auto r = call(c, "GET", "/plans/" + sdk::url_encode(plan));
+    if (r.status != 200 && r.status != 202 && r.status != 417) return emit(r);
+    if (c.json) {
+      std::cout << sdk::Json::parse(r.body).dump(2) << std::endl;
+    } else {
+      std::cout << plan_tree(plan, sdk::Json::parse(r.body)) << std::endl;
+    }
+    return 0;
+  }
+  std::string plan = arg(a, 1);
+  if (plan.empty()) die("missing PLAN argument");
+  std::string p = "/plans/" + sdk::url_encode(plan);
+  if (cmd == "start") {
+    sdk::Json params = sdk::Json::object();
+    for (size_t i = 2; i < a.size(); ++i) {
+      if ((a[i] == "-p" || a[i] == "--params") && i + 1 < a.size()) {
+        std::string kv = a[++i];
+        size_t eq = kv.find('=');
+        if (eq == std::string::npos) die("parameters must be KEY=VALUE: " + kv);
+        params.set(kv.substr(0, eq), sdk::Json(kv.substr(eq + 1)));
+      }
+    }
+    return emit(call(c, "POST", p + "/start", params.dump()));
+  }
+  if (cmd == "stop") return emit(call(c, "POST", p + "/stop"));
+  if (cmd == "pause") return emit(call(c, "POST", p + "/interrupt" + query({{"phase", arg(a, 2)}})));
+  if (cmd == "resume") return emit(call(c, "POST", p + "/continue" + query({{"phase", arg(a, 2)}})));
+  if (cmd == "force-restart")
+    return emit(call(c, "POST", p + "/restart" + query({{"phase", arg(a, 2)}, {"step", arg(a, 3)}})));
+  if (cmd == "force-complete")
+    return emit(call(c, "POST", p + "/forceComplete" + query({{"phase", arg(a, 2)}, {"step", arg(a, 3)}})));
+  usage();
+  return 1;
+}
+
+std::string task_filter(const std::vector<std::string>& a, size_t from) {
+  sdk::Json tasks = sdk::Json::array();
+  for (size_t i = from; i < a.size(); ++i)
+    if ((a[i] == "-t" || a[i] == "--tasks") && i + 1 < a.size()) tasks.push(sdk::Json(a[++i]));
+  return tasks.size() ? tasks.dump() : "";
+}
+
+int pod_cmd(Ctx& c, const std::vector<std::string>& a) {
+  std::string cmd = arg(a, 0);
+  if (cmd == "list") return emit(call(c, "GET", "/pod"));
+  if (cmd == "status") {
+    std::string pod = arg(a, 1);
+    auto r = call(c, "GET", pod.empty() ? "/pod/status" : "/pod/" + sdk::url_encode(pod) + "/status");
+    if (r.status != 200 || c.json) return emit(r);
+    auto j = sdk::Json::parse(r.body);
+    if (pod.empty()) {
+      std::cout << pods_tree(j) << std::endl;
+    } else {
+      std::string out = or_unknown(j["name"]) + "\n";
+      append_tasks(out, j["tasks"], "");
+      while (!out.empty() && out.back() == '\n') out.pop_back();
+      std::cout << out << std::endl;
+    }
+    return 0;
+  }
+  std::string pod = arg(a, 1);
+  if (pod.empty()) die("missing POD argument");
+  std::string p = "/pod/" + sdk::url_encode(pod);
+  if (cmd == "info") return emit(call(c, "GET", p + "/info"));
+  if (cmd == "restart") return emit(call(c, "POST", p + "/restart"));
+  if (cmd == "replace") return emit(call(c, "POST", p + "/replace"));
+  if (cmd == "pause") return emit(call(c, "POST", p + "/pause", task_filter(a, 2)));
+  if (cmd == "resume") return emit(call(c, "POST", p + "/resume", task_filter(a, 2)));
+  usage();
+  return 1;
+}
+
+int debug_cmd(Ctx& c, const std::vector<std::string>& a) {
+  std::string sec = arg(a, 0), cmd = arg(a, 1);
+  if (sec == "config") {
+    if (cmd == "list") return emit(call(c, "GET", "/configurations"));
+    if (cmd == "show") return emit(call(c, "GET", "/configurations/" + sdk::url_encode(arg(a, 2))));
+    if (cmd == "target") return emit(call(c, "GET", "/configurations/target"));
+    if (cmd == "target_id") return emit(call(c, "GET", "/configurations/targetId"));
+  } else if (sec == "state") {
+    if (cmd == "framework_id") return emit(call(c, "GET", "/state/frameworkId"));
+    if (cmd == "properties") return emit(call(c, "GET", "/state/properties"));
+    if (cmd == "property") return emit(call(c, "GET", "/state/properties/" + sdk::url_encode(arg(a, 2))), false);
+    if (cmd == "refresh_cache") return emit(call(c, "PUT", "/state/refresh"));
+  } else if (sec == "pod") {
+    std::vector<std::string> rest(a.begin() + 1, a.end());
+    return pod_cmd(c, rest);
+  } else if (sec == "plans" || sec == "offers" || sec == "taskStatuses" || sec == "reservations") {
+    return emit(call(c, "GET", "/debug/" + sec));
+  }
+  usage();
+  return 1;
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  Ctx c;
+  std::string url = std::getenv("SDK_SCHEDULER_URL") ? std::getenv("SDK_SCHEDULER_URL") : "http://127.0.0.1:8080";
+  if (const char* tok = std::getenv("DCOS_AUTH_TOKEN")) c.headers["Authorization"] = std::string("token=") + tok;
+  std::vector<std::string> a;
+  for (int i = 1; i < argc; ++i) {
+    std::string s = argv[i];
+    if (s == "--url" && i + 1 < argc) url = argv[++i];
+    else if (s.rfind("--url=", 0) == 0) url = s.substr(6);
+    else if ((s == "--service" || s == "--name") && i + 1 < argc) c.service = argv[++i];
+    else if (s.rfind("--service=", 0) == 0) c.service = s.substr(10);
+    else if (s == "--json") c.json = true;
+    else if (s == "-h" || s == "--help") { usage(); return 0; }
+    else a.push_back(s);
+  }
+  try {
+    c.base = sdk::parse_url(url);
+  } catch (const std::exception& e) {
+    die(e.what());
+  }
+  if (a.empty()) {
+    usage();
+    return 1;
+  }
+  std::string section = a[0];
+  std::vector<std::string> rest(a.begin() + 1, a.end());
+  try {
+    if (section == "plan") return plan_cmd(c, rest);
+    if (section == "pod") return pod_cmd(c, rest);
+    if (section == "endpoints")
+      return emit(call(c, "GET", rest.empty() ? "/endpoints" : "/endpoints/" + sdk::url_encode(rest[0])));
+    if (section == "debug") return debug_cmd(c, rest);
+    if (section == "describe") return emit(call(c, "GET", "/configurations/target"));
+    if (section == "update" && arg(rest, 0) == "status") {
+      std::vector<std::string> r2 = {"status", "deploy"};
+      return plan_cmd(c, r2);
+    }
+    if (section == "health") return emit(call(c, "GET", "/health?verbose=true"));
+    if (section == "metrics") return emit(call(c, "GET", "/metrics"));
+  } catch (const sdk::JsonError& e) {
+    die(std::string("Unexpected response: ") + e.what());
+  }
+  usage();
+  return 1;
+}
