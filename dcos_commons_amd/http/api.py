@@ -98,7 +98,8 @@ class Route:
     regex: "re.Pattern" = None
 
     def __post_init__(self):
-        pattern = re.sub(r"\{(\w+)\}", r"(?P<\1>[^/]+)", self.template.rstrip("/") or "/")
+        pattern = re.sub(r"\{(\w+):path\}", r"(?P<\1>.+)", self.template.rstrip("/") or "/")
+        pattern = re.sub(r"\{(\w+)\}", r"(?P<\1>[^/]+)", pattern)
         self.regex = re.compile("^" + pattern + "/?$")
 
 
