@@ -80,7 +80,10 @@ class FrameworkRunner:
         if master.startswith("http://") or master.startswith("https://"):
             from dcos_commons_amd.mesos.http_driver import V1HttpSchedulerDriver
 
-            return lambda sched, info: V1HttpSchedulerDriver(master, sched, info)
+            cfg = self.scheduler_config
+            return lambda sched, info: V1HttpSchedulerDriver(
+                master, sched, info, credential=cfg.mesos_credential(), content_type=cfg.mesos_content_type(),
+                reconnect=cfg.is_driver_reconnect())
         from dcos_commons_amd.mesos.local_master import LocalSchedulerDriver, local_master_from_env
 
         lm = local_master_from_env(self.scheduler_config.env)

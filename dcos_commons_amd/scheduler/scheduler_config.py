@@ -153,6 +153,23 @@ class SchedulerConfig:
         """MI355X build: the v1 HTTP endpoint of the master (``SDK_MESOS_MASTER``)."""
         return self.env.get_optional("SDK_MESOS_MASTER", "http://leader.mesos:5050")
 
+    def mesos_content_type(self) -> str:
+        """``protobuf`` (default) or ``json`` body encoding on the v1 scheduler API."""
+        v = self.env.get_optional("SDK_MESOS_CONTENT_TYPE", "protobuf").lower()
+        return "application/json" if v == "json" else "application/x-protobuf"
+
+    def is_driver_reconnect(self) -> bool:
+        """MI355X build: resubscribe after a lost event stream instead of exiting (reference exits)."""
+        return self.env.get_optional_boolean("SDK_DRIVER_RECONNECT", False)
+
+    def mesos_credential(self):
+        principal = self.env.get_optional("SDK_MESOS_PRINCIPAL", "")
+        if not principal:
+            return None
+        from dcos_commons_amd.mesos import protos as P
+
+        return P.Credential(principal=principal, secret=self.env.get_optional("SDK_MESOS_SECRET", ""))
+
     def pause_override_cmd(self) -> str:
         return self.env.get_optional("PAUSE_OVERRIDE_CMD", PAUSE_COMMAND)
 

@@ -31,7 +31,7 @@ def hello_env(hello=2, world=2):
 
 
 class Cluster:
-    def __init__(self, spec_file="svc.yml", agents=3, gpus=0, env=None, **cfg):
+    def __init__(self, spec_file="svc.yml", agents=3, gpus=0, env=None, transport="local", **cfg):
         self.env = env or hello_env()
         overrides = {"PORT_API": "0", "SDK_OFFER_WAIT_S": "0.5"}
         overrides.update(cfg)
@@ -42,8 +42,18 @@ class Cluster:
         self.agent_ids = [self.master.add_agent(AgentSpec(hostname=f"host-{i}", cpus=4, mem=8192, disk=20000,
                                                           gpus=gpus)) for i in range(agents)]
         self.persister = MemPersister()
+        self.http_master = None
+        if transport == "local":
+            factory = lambda s, i: LocalSchedulerDriver(self.master, s, i)  # noqa: E731
+        else:  # the Mesos v1 HTTP API, over a socket, in json or protobuf
+            from dcos_commons_amd.mesos.http_driver import JSON, PROTOBUF, V1HttpSchedulerDriver
+            from dcos_commons_amd.mesos.http_master import HttpMaster
+
+            self.http_master = HttpMaster(self.master, heartbeat_s=1.0).start()
+            ctype = JSON if transport == "json" else PROTOBUF
+            factory = lambda s, i: V1HttpSchedulerDriver(self.http_master.url, s, i, content_type=ctype)  # noqa: E731
         self.runner = SchedulerRunner(SchedulerBuilder(self.spec, self.cfg, self.persister).set_plans_from(raw),
-                                      driver_factory=lambda s, i: LocalSchedulerDriver(self.master, s, i))
+                                      driver_factory=factory)
 
     def __enter__(self):
         self.runner.run(block=False)
@@ -53,6 +63,8 @@ class Cluster:
 
     def __exit__(self, *exc):
         self.runner.stop()
+        if self.http_master is not None:
+            self.http_master.stop()
         self.master.shutdown()
 
     def wait(self, pred, timeout=20.0):

@@ -1,0 +1,238 @@
+"""Mesos v1 HTTP scheduler API: RecordIO codec, driver <-> master wire contract, and the full
+helloworld scheduler deployed/recovered over a socket (SURVEY §2.10 "libmesos /
+mesos-http-adapter" row; reference driver selection in framework/SchedulerDriverFactory.java)."""
+import http.client
+import json
+import threading
+import time
+
+import pytest
+
+from dcos_commons_amd.framework.process_exit import ProcessExit
+from dcos_commons_amd.mesos import protos as P
+from dcos_commons_amd.mesos import recordio
+from dcos_commons_amd.mesos.http_driver import JSON, PROTOBUF, V1HttpSchedulerDriver, encode_message
+from dcos_commons_amd.mesos.http_master import HttpMaster
+from dcos_commons_amd.mesos.local_master import AgentSpec, LocalMaster
+from test_e2e_helloworld import Cluster
+
+
+def test_recordio_roundtrip_and_partial_feeds():
+    recs = [b"", b"a", b"hello\nworld", bytes(range(256)) * 40]
+    wire = b"".join(recordio.encode(r) for r in recs)
+    for step in (1, 3, 7, 4096, len(wire)):
+        dec = recordio.Decoder()
+        out = []
+        for i in range(0, len(wire), step):
+            out.extend(dec.feed(wire[i:i + step]))
+        assert out == recs and dec.pending_bytes == 0
+    with pytest.raises(recordio.RecordIOError):
+        recordio.Decoder().feed(b"12x\n")
+    with pytest.raises(recordio.RecordIOError):
+        recordio.Decoder(max_record_bytes=4).feed(b"5\nabcde")
+    chunks = iter([wire[:5], wire[5:], b""])
+    assert list(recordio.iter_records(lambda n: next(chunks))) == recs
+    bad = iter([b"10\nabc", b""])
+    with pytest.raises(recordio.RecordIOError):
+        list(recordio.iter_records(lambda n: next(bad)))
+
+
+class Recorder:
+    def __init__(self):
+        self.events = []
+        self.cv = threading.Condition()
+
+    def _add(self, *e):
+        with self.cv:
+            self.events.append(e)
+            self.cv.notify_all()
+
+    def registered(self, d, fid, mi):
+        self._add("registered", fid.value)
+
+    def reregistered(self, d, mi):
+        self._add("reregistered")
+
+    def resource_offers(self, d, offers):
+        self._add("offers", offers)
+
+    def offer_rescinded(self, d, oid):
+        self._add("rescind", oid.value)
+
+    def status_update(self, d, st):
+        self._add("update", st)
+
+    def disconnected(self, d):
+        self._add("disconnected")
+
+    def error(self, d, msg):
+        self._add("error", msg)
+
+    def wait_for(self, kind, n=1, timeout=10):
+        with self.cv:
+            ok = self.cv.wait_for(lambda: sum(1 for e in self.events if e[0] == kind) >= n, timeout)
+        assert ok, f"no {kind} event; have {[e[0] for e in self.events]}"
+        return [e for e in self.events if e[0] == kind]
+
+
+@pytest.fixture
+def cluster():
+    lm = LocalMaster(allocation_interval_s=0.05)
+    lm.add_agent(AgentSpec(hostname="h0", cpus=2, mem=1024, disk=1000))
+    hm = HttpMaster(lm, heartbeat_s=0.2).start()
+    yield lm, hm
+    hm.stop()
+    lm.shutdown()
+
+
+@pytest.mark.parametrize("ctype", [PROTOBUF, JSON])
+def test_subscribe_offers_launch_kill_ack(cluster, ctype):
+    lm, hm = cluster
+    rec = Recorder()
+    d = V1HttpSchedulerDriver(hm.url, rec, P.FrameworkInfo(name="fw", role="r", user="u"), content_type=ctype)
+    d.start()
+    try:
+        fid = rec.wait_for("registered")[0][1]
+        assert d.framework_id == fid and d.stream_id
+        offer = rec.wait_for("offers")[0][1][0]
+        assert offer.hostname == "h0"
+        op = P.Offer.Operation(type=P.Offer.Operation.LAUNCH)
+        t = op.launch.task_infos.add(name="t")
+        t.task_id.value = "t-1"
+        t.agent_id.CopyFrom(offer.agent_id)
+        t.command.value = "sleep 1000"
+        t.resources.extend([r for r in offer.resources if r.name == "cpus"])
+        d.accept_offers([offer.id], [op], P.Filters(refuse_seconds=1))
+        wait_state = lambda s: any(e[1].state == s for e in rec.wait_for("update"))  # noqa: E731
+        deadline = time.time() + 10
+        while not wait_state(P.TASK_RUNNING) and time.time() < deadline:
+            time.sleep(0.01)
+        assert lm.task_states()["t-1"] == P.TASK_RUNNING
+        d.kill_task(P.TaskID(value="t-1"))
+        deadline = time.time() + 10
+        while lm.task_states().get("t-1") != P.TASK_KILLED and time.time() < deadline:
+            time.sleep(0.01)
+        assert lm.task_states()["t-1"] == P.TASK_KILLED
+        # every status that carried a uuid was implicitly acknowledged
+        time.sleep(0.1)
+        sub = hm.subscriptions[fid]
+        uuids = {e[1].uuid for e in rec.events if e[0] == "update" and e[1].uuid}
+        assert uuids and uuids <= set(sub.acknowledged)
+        d.reconcile_tasks([P.TaskStatus(task_id=P.TaskID(value="nope"), state=P.TASK_RUNNING)])
+        deadline = time.time() + 5
+        while not any(e[0] == "update" and e[1].task_id.value == "nope" for e in rec.events) and time.time() < deadline:
+            time.sleep(0.01)
+        lost = [e[1] for e in rec.events if e[0] == "update" and e[1].task_id.value == "nope"]
+        assert lost and lost[0].state == P.TASK_LOST
+        d.suppress_offers()
+        d.revive_offers()
+        time.sleep(0.5)  # heartbeats (0.2 s) keep the stream alive
+        assert not any(e[0] == "disconnected" for e in rec.events)
+        assert hm.calls["ACCEPT"] == 1 and hm.calls["KILL"] == 1 and hm.calls["ACKNOWLEDGE"] >= 1
+    finally:
+        d.stop()
+
+
+def test_calls_need_current_stream_id(cluster):
+    lm, hm = cluster
+    rec = Recorder()
+    d = V1HttpSchedulerDriver(hm.url, rec, P.FrameworkInfo(name="fw", role="r"))
+    d.start()
+    try:
+        fid = rec.wait_for("registered")[0][1]
+        conn = http.client.HTTPConnection("127.0.0.1", hm.port, timeout=5)
+        call = P.Call(type=P.Call.REVIVE)
+        call.framework_id.value = fid
+        conn.request("POST", "/api/v1/scheduler", body=encode_message(call, JSON),
+                     headers={"Content-Type": JSON, "Mesos-Stream-Id": "bogus"})
+        r = conn.getresponse()
+        r.read()
+        assert r.status == 400
+        conn.request("POST", "/api/v1/scheduler", body=b"{", headers={"Content-Type": JSON})
+        r = conn.getresponse()
+        r.read()
+        assert r.status == 400
+        conn.request("GET", "/state")
+        r = conn.getresponse()
+        state = json.loads(r.read())
+        assert state["frameworks"] == [fid] and state["agents"][0]["hostname"] == "h0"
+    finally:
+        d.stop()
+
+
+def test_redirect_to_leader(cluster):
+    lm, hm = cluster
+    follower = HttpMaster(lm, redirect_to=hm.url).start()
+    rec = Recorder()
+    d = V1HttpSchedulerDriver(follower.url, rec, P.FrameworkInfo(name="fw", role="r"))
+    d.start()
+    try:
+        rec.wait_for("registered")
+        assert d.master_url == hm.url
+        d.revive_offers()
+    finally:
+        d.stop()
+        follower.stop()
+
+
+def test_stream_loss_disconnects_or_fails_over(cluster):
+    lm, hm = cluster
+    rec = Recorder()
+    d = V1HttpSchedulerDriver(hm.url, rec, P.FrameworkInfo(name="fw", role="r"))
+    d.start()
+    rec.wait_for("registered")
+    hm.drop_streams()
+    rec.wait_for("disconnected")  # reference semantics: the scheduler exits on disconnection
+    assert d.join(5) and d.exit_status == 5
+
+    rec2 = Recorder()
+    d2 = V1HttpSchedulerDriver(hm.url, rec2, P.FrameworkInfo(name="fw2", role="r"), reconnect=True, backoff_s=0.05)
+    d2.start()
+    try:
+        fid = rec2.wait_for("registered")[0][1]
+        old_stream = d2.stream_id
+        hm.drop_streams()
+        rec2.wait_for("reregistered")
+        assert d2.framework_id == fid and d2.stream_id != old_stream  # same framework, new stream
+        d2.revive_offers()
+        # a second subscriber with the same FrameworkID takes over; the first gets ERROR
+        rec3 = Recorder()
+        info = P.FrameworkInfo(name="fw2", role="r")
+        info.id.value = fid
+        d3 = V1HttpSchedulerDriver(hm.url, rec3, info)
+        d3.start()
+        rec3.wait_for("registered")
+        rec2.wait_for("error")
+        d3.stop(failover=False)  # TEARDOWN removes the framework
+        deadline = time.time() + 5
+        while fid in lm.frameworks and time.time() < deadline:
+            time.sleep(0.01)
+        assert fid not in lm.frameworks
+    finally:
+        d2.stop()
+
+
+def test_subscribe_rejected_calls_error():
+    rec = Recorder()
+    d = V1HttpSchedulerDriver("http://127.0.0.1:9", rec, P.FrameworkInfo(name="fw"), backoff_s=0.01,
+                              max_backoff_s=0.02)
+    d.start()
+    time.sleep(0.2)  # connection refused: keeps retrying (no leader yet), never registers
+    assert not rec.events
+    d.stop()
+    assert d.join(1)
+
+
+@pytest.mark.parametrize("transport", ["protobuf", "json"])
+def test_helloworld_over_http(transport):
+    ProcessExit.set_test_mode(True)
+    with Cluster(transport=transport) as c:
+        c.wait_plan("deploy")
+        states = c.master.task_states()
+        assert len(states) == 4 and set(states.values()) == {P.TASK_RUNNING}
+        old = c.store.fetch_task("hello-0-server").task_id.value
+        c.master.fail_task(old)
+        c.wait(lambda: c.store.fetch_status("hello-0-server").task_id.value != old and
+               c.store.fetch_status("hello-0-server").state == P.TASK_RUNNING)
+        c.wait_plan("recovery")
+        assert c.http_master.calls["ACCEPT"] >= 5
