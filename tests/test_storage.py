@@ -12,9 +12,25 @@ from dcos_commons_amd.storage.persister import PersisterException, Reason
 from dcos_commons_amd.storage.persister_cache import PersisterCache
 
 
-@pytest.fixture(params=["mem", "file", "cache-mem", "cache-file"])
+@pytest.fixture(scope="module")
+def zk_server():
+    from dcos_commons_amd.testing.zk_server import ZkServer
+
+    srv = ZkServer().start()
+    yield srv
+    srv.stop()
+
+
+@pytest.fixture(params=["mem", "file", "cache-mem", "cache-file", "zk", "cache-zk"])
 def persister(request, tmp_path):
     kind = request.param
+    if kind in ("zk", "cache-zk"):
+        from dcos_commons_amd.storage.zk_persister import ZooKeeperPersister
+
+        zk = request.getfixturevalue("zk_server")
+        p = ZooKeeperPersister(zk.connect_string, "/test/" + request.node.name.replace("[", "-").rstrip("]"))
+        request.addfinalizer(p.close)
+        return PersisterCache(p) if kind == "cache-zk" else p
     if kind == "mem":
         return MemPersister()
     if kind == "file":
