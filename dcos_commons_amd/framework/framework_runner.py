@@ -77,8 +77,10 @@ class FrameworkRunner:
 
     def _default_driver_factory(self):
         master = self.scheduler_config.mesos_master_url()
-        if master.startswith("http://") or master.startswith("https://"):
-            from dcos_commons_amd.mesos.http_driver import V1HttpSchedulerDriver
+        if master.startswith(("http://", "https://", "zk://")):
+            from dcos_commons_amd.mesos.http_driver import V1HttpSchedulerDriver, resolve_master_url
+
+            master = resolve_master_url(master)
 
             cfg = self.scheduler_config
             return lambda sched, info: V1HttpSchedulerDriver(

@@ -29,6 +29,7 @@ import json
 import logging
 import socket
 import threading
+import time
 import urllib.parse
 from typing import Iterable, List, Optional
 
@@ -387,3 +388,35 @@ class V1HttpSchedulerDriver(SchedulerDriver):
             pass
         else:
             LOGGER.debug("Ignoring event type %s", t)
+
+
+def resolve_master_url(url: str, timeout_s: float = 10.0) -> str:
+    """``http(s)://host:port`` as is; ``zk://hosts/path`` -> the leading master's v1 endpoint.
+
+    Mesos masters publish ephemeral-sequential ``json.info_<seq>`` nodes (MasterInfo as JSON)
+    under the ZK path; the lowest sequence number is the leader (how libmesos' detector, used by
+    the reference's ``zk://master.mesos:2181/mesos`` driver URL, finds it).
+    """
+    if not url.startswith("zk://"):
+        return url
+    from dcos_commons_amd.storage import zookeeper as Z
+
+    rest = url[len("zk://"):]
+    hosts, _, path = rest.partition("/")
+    client = Z.ZkClient(hosts, connect_timeout_s=timeout_s).start()
+    try:
+        deadline = time.monotonic() + timeout_s
+        while True:
+            infos = sorted(c for c in client.get_children("/" + path) if c.startswith("json.info_"))
+            if infos:
+                data, _ = client.get(f"/{path}/{infos[0]}")
+                info = json.loads((data or b"{}").decode("utf-8"))
+                addr = info.get("address") or {}
+                host = addr.get("hostname") or addr.get("ip") or info.get("hostname")
+                port = addr.get("port") or info.get("port") or 5050
+                return f"http://{host}:{port}"
+            if time.monotonic() > deadline:
+                raise MesosCallError(503, f"no leading master registered under {url}")
+            time.sleep(0.1)
+    finally:
+        client.close()

@@ -132,8 +132,23 @@ class HttpMaster:
             subs = list(self.subscriptions.values())
         for s in subs:
             s.close()
+        if getattr(self, "_zk", None) is not None:
+            self._zk.close()
         self.httpd.shutdown()
         self.httpd.server_close()
+
+    def register_in_zk(self, connect: str, path: str = "/mesos"):
+        """Publishes this master as ``<path>/json.info_<seq>`` (ephemeral), like a Mesos leader."""
+        from dcos_commons_amd.storage import zookeeper as Z
+
+        client = Z.ZkClient(connect).start()
+        client.ensure_path(path)
+        host, port = self.httpd.server_address[:2]
+        info = {"id": self.master.master_info.id, "hostname": host, "port": port,
+                "address": {"hostname": host, "ip": host, "port": port}}
+        client.create(path + "/json.info_", json.dumps(info).encode(), ephemeral=True, sequence=True)
+        self._zk = client
+        return client
 
     def drop_streams(self) -> None:
         """Closes every event stream (simulates a master failover / network cut)."""

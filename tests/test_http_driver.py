@@ -236,3 +236,26 @@ def test_helloworld_over_http(transport):
                c.store.fetch_status("hello-0-server").state == P.TASK_RUNNING)
         c.wait_plan("recovery")
         assert c.http_master.calls["ACCEPT"] >= 5
+
+
+def test_zk_master_detection(cluster):
+    from dcos_commons_amd.mesos.http_driver import resolve_master_url
+    from dcos_commons_amd.testing.zk_server import ZkServer
+
+    lm, hm = cluster
+    zk = ZkServer().start()
+    try:
+        assert resolve_master_url("http://x:1") == "http://x:1"
+        standby = HttpMaster(lm, redirect_to=hm.url).start()
+        hm.register_in_zk(zk.connect_string, "/mesos")  # first registered = leader
+        standby.register_in_zk(zk.connect_string, "/mesos")
+        url = resolve_master_url(f"zk://{zk.connect_string}/mesos")
+        assert url == hm.url
+        rec = Recorder()
+        d = V1HttpSchedulerDriver(url, rec, P.FrameworkInfo(name="fw", role="r"))
+        d.start()
+        rec.wait_for("registered")
+        d.stop()
+        standby.stop()
+    finally:
+        zk.stop()
