@@ -476,3 +476,71 @@ class DestroyEvaluationStage(OfferEvaluationStage):
         return EvaluationOutcome.pass_(self, "Destroying orphaned resource: %s", P.to_text(self.resource),
                                        recommendations=[DestroyOfferRecommendation(pool.offer, self.resource)],
                                        mesos_resource=MesosResource(self.resource))
+
+
+# ---------------------------------------------------------------------------------------
+# TLSEvaluationStage
+
+
+class TLSEvaluationStage(OfferEvaluationStage):
+    """Provisions the task's TLS artifacts as secrets and mounts them read-only in the container.
+
+    Reference: offer/evaluate/TLSEvaluationStage.java:110-190. Artifacts are (re)generated only when
+    a secret is missing (e.g. the SANs changed); each transport-encryption entry mounts
+    ``<name>.crt/.key/.ca`` (TLS) or ``<name>.keystore/.truststore`` (KEYSTORE) as SECRET volumes.
+    """
+
+    class Builder:
+        def __init__(self, service_name: str, scheduler_config, updater=None):
+            self.service_name = service_name
+            self.scheduler_config = scheduler_config
+            self.namespace = scheduler_config.secrets_namespace(service_name)
+            if updater is None:
+                from dcos_commons_amd.dcos.clients import CertificateAuthorityClient, DcosHttpExecutor, SecretsClient
+                from dcos_commons_amd.offer.evaluate.security import TLSArtifactsGenerator, TLSArtifactsUpdater
+
+                executor = DcosHttpExecutor(scheduler_config.dcos_auth_token_provider())
+                updater = TLSArtifactsUpdater(service_name, SecretsClient(executor),
+                                              TLSArtifactsGenerator(CertificateAuthorityClient(executor)))
+            self.updater = updater
+
+        def build(self, task_name: str) -> "TLSEvaluationStage":
+            return TLSEvaluationStage(self.service_name, task_name, self.namespace, self.updater,
+                                      self.scheduler_config)
+
+        __call__ = build
+
+    def __init__(self, service_name: str, task_name: str, namespace: str, updater, scheduler_config):
+        self.service_name = service_name
+        self.task_name = task_name
+        self.namespace = namespace
+        self.updater = updater
+        self.scheduler_config = scheduler_config
+
+    def evaluate(self, pool: MesosResourcePool, builder: PodInfoBuilder) -> EvaluationOutcome:
+        from dcos_commons_amd.offer.evaluate.security import CertificateNamesGenerator, TLSArtifactPaths
+
+        pi = builder.pod_instance
+        task_spec = next(t for t in pi.pod.tasks if t.name == self.task_name)
+        if not task_spec.transport_encryption:
+            return EvaluationOutcome.pass_(self, "No TLS specs found for task")
+        names = CertificateNamesGenerator(self.service_name, task_spec, pi, self.scheduler_config)
+        paths = TLSArtifactPaths(self.namespace, common_id_utils.get_task_instance_name(pi, task_spec),
+                                 names.sans_hash())
+        task = builder.get_task_builder(self.task_name)
+        for te in task_spec.transport_encryption:
+            try:
+                self.updater.update(paths, names, te.name)
+            except Exception as e:  # noqa: BLE001
+                LOGGER.error("Failed to process certificates for %s: %s", self.task_name, e)
+                return EvaluationOutcome.fail(
+                    self, "Failed to store TLS artifacts for task %s because of exception: %s", self.task_name, e)
+            existing = {(v.container_path, v.source.secret.reference.name) for v in task.container.volumes}
+            for entry in paths.get_paths_for_type(te.type.value, te.name):
+                if (entry.mount_path, entry.secret_store_path) in existing:
+                    continue
+                v = task.container.volumes.add(container_path=entry.mount_path, mode=P.Volume.RO)
+                v.source.type = P.Volume.Source.SECRET
+                v.source.secret.type = P.Secret.REFERENCE
+                v.source.secret.reference.name = entry.secret_store_path
+        return EvaluationOutcome.pass_(self, "TLS certificate created and added to the task")

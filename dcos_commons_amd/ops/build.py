@@ -64,11 +64,11 @@ def build_probe_binary(force: bool = False, verbose: bool = False) -> str:
 
 
 def build_cpp_tools(force: bool = False, verbose: bool = False) -> List[str]:
-    """CMake build of the C++ natives (bootstrap, CLI) if their sources exist."""
+    """CMake build of the C++ natives (bootstrap, CLI, TLS crypto library) if their sources exist."""
     if not os.path.exists(os.path.join(NATIVE, "CMakeLists.txt")):
         return []
     os.makedirs(BUILD, exist_ok=True)
-    targets = [os.path.join(BUILD, n) for n in ("sdk-bootstrap", "sdk-cli")]
+    targets = [os.path.join(BUILD, n) for n in ("sdk-bootstrap", "sdk-cli", "native-tests", "libsdktls.so")]
     srcs = []
     for d, _, fs in os.walk(NATIVE):
         if os.path.abspath(d).startswith(os.path.abspath(BUILD)):

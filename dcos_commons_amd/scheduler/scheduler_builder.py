@@ -38,6 +38,7 @@ from dcos_commons_amd.scheduler.recovery import (
     NeverFailureMonitor,
     TimedFailureMonitor,
 )
+from dcos_commons_amd.offer.task_utils import has_tasks_with_tls
 from dcos_commons_amd.scheduler.uninstall import UninstallScheduler
 from dcos_commons_amd.specification.specs import ServiceSpec, ServiceSpecFactory, loopback_check
 from dcos_commons_amd.state import state_store_utils
@@ -189,9 +190,15 @@ class SchedulerBuilder:
                                                               self.scheduler_config, prefix=spec.name)
         else:
             url_factory = endpoint_utils.template_url_factory(spec.name, self.scheduler_config)
+        tls_factory = self.tls_stage_factory
+        if tls_factory is None and has_tasks_with_tls(spec):
+            # OfferEvaluator.java:287: the TLS stage builder exists only when some task wants TLS
+            from dcos_commons_amd.offer.evaluate.stages import TLSEvaluationStage
+
+            tls_factory = TLSEvaluationStage.Builder(spec.name, self.scheduler_config)
         return DefaultScheduler(spec, self.scheduler_config, namespace, self.custom_resources, coordinator,
                                 self.plan_customizer, framework_store, state_store, config_store, url_factory,
-                                self.endpoint_producers, self.tls_stage_factory)
+                                self.endpoint_producers, tls_factory)
 
     def _recovery_plan_manager(self, spec, state_store, config_store, plans, namespace):
         overriders = []

@@ -134,6 +134,16 @@ class SchedulerConfig:
     def side_channel_credential(self) -> Optional[str]:
         return self.env.get_optional("DCOS_SERVICE_ACCOUNT_CREDENTIAL", None)
 
+    def dcos_auth_token_provider(self):
+        """Cached IAM token provider for the service account (SchedulerConfig.java:484-523)."""
+        from dcos_commons_amd.dcos.clients import ConstantTokenProvider, token_provider_from_service_account
+
+        static = self.env.get_optional("SDK_DCOS_AUTH_TOKEN", None)
+        if static:
+            return ConstantTokenProvider(static)
+        return token_provider_from_service_account(self.env.get_required("DCOS_SERVICE_ACCOUNT_CREDENTIAL"),
+                                                   self.auth_token_refresh_threshold_s())
+
     # statsd
     def statsd_poll_interval_s(self) -> int:
         return self.env.get_optional_long("STATSD_POLL_INTERVAL_S", 10)

@@ -237,6 +237,15 @@ class UninstallScheduler:
             self.logger.info("Service has been told to uninstall. Marking this in the persistent state store. "
                              "Uninstall cannot be canceled once triggered.")
             state_store_utils.set_uninstalling(state_store)
+        if secrets_client is None and has_tasks_with_tls(service_spec):
+            # UninstallScheduler.java:90-105: TLS secrets are cleaned up with the service account's token
+            try:
+                from dcos_commons_amd.dcos.clients import DcosHttpExecutor, SecretsClient
+
+                secrets_client = SecretsClient(DcosHttpExecutor(scheduler_config.dcos_auth_token_provider()))
+            except Exception as e:  # noqa: BLE001
+                self.logger.error("Failed to create a secrets store client, TLS artifacts possibly won't be "
+                                  "cleaned up from secrets store: %s", e)
         factory = UninstallPlanFactory(service_spec, state_store, scheduler_config, namespace, secrets_client)
         self.recorder = UninstallRecorder(state_store, factory.resource_cleanup_steps)
         self.deregister_step = factory.deregister_step
