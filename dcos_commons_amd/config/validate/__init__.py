@@ -218,7 +218,11 @@ class TLSRequiresServiceAccount(ConfigValidator):
         self.scheduler_config = scheduler_config
 
     def validate(self, old, new):
-        if has_tasks_with_tls(new) and not self.scheduler_config.is_side_channel_active():
+        if not has_tasks_with_tls(new):
+            return []
+        try:
+            self.scheduler_config.dcos_auth_token_provider()  # construction only; no login happens here
+        except Exception:  # noqa: BLE001
             return [ConfigValidationError.value_error(
                 "transport-encryption", "",
                 "Scheduler is missing a service account that is required for provisioning TLS artifacts. "

@@ -167,6 +167,12 @@ _MISSING = object()
 def _lookup(stack: List[Any], name: str):
     if name == ".":
         return stack[-1]
+    if "." in name:
+        # jmustache (non-standards mode) tries the whole key first: Universe options are
+        # flattened to keys like "service.user" (CosmosRenderer.flattenPropertyTree).
+        for ctx in reversed(stack):
+            if isinstance(ctx, Mapping) and name in ctx:
+                return ctx[name]
     parts = name.split(".")
     for ctx in reversed(stack):
         if isinstance(ctx, Mapping) and parts[0] in ctx:

@@ -2,6 +2,7 @@
 from __future__ import annotations
 
 import os
+import random
 import uuid
 from dataclasses import dataclass, field
 from typing import Callable, Dict, Iterable, List, Optional
@@ -190,6 +191,13 @@ class SendOffer(Send):
         self.agent_id: Optional[str] = None
         self.extra: List[P.Resource] = []
         self.attributes: Dict[str, str] = {}
+        self.with_unreserved = False
+
+    def add_unreserved_resources(self) -> "SendOffer":
+        """With a reoffer: also include unreserved resources for the pod type (e.g. for sidecar tasks
+        with their own resource set that launch next to an existing executor)."""
+        self.with_unreserved = True
+        return self
 
     def set_pod_index_to_reoffer(self, index: int) -> "SendOffer":
         self.pod_to_reuse = f"{self.pod_type}-{index}"
@@ -244,9 +252,15 @@ class SendOffer(Send):
             by_id: Dict[str, P.Resource] = {}
             executors = set()
             for a in sim.state.accepts_for_pod(self.pod_to_reuse):
+                # every reservation made for the pod (incl. resource sets of tasks not launched yet),
+                # superseded below by launched tasks' copies, which carry volume persistence
+                for op in a.of_type(Op.RESERVE):
+                    for r in op.reserve.resources:
+                        by_id[get_resource_id(r) or str(uuid.uuid4())] = r
                 for e in a.executors():
                     for r in e.resources:
                         by_id[get_resource_id(r) or str(uuid.uuid4())] = r
+                    executors.add(e.executor_id.value)
                 for t in a.launched_tasks():
                     if not t.name.startswith(self.pod_to_reuse + "-"):
                         continue
@@ -256,9 +270,9 @@ class SendOffer(Send):
                         by_id[rid or str(uuid.uuid4())] = r
                     executors.add(t.executor.executor_id.value)
             o.resources.extend(by_id.values())
-            for e in sorted(executors):
+            for e in sorted(x for x in executors if x):
                 o.executor_ids.add(value=e)
-        else:
+        if not self.pod_to_reuse or self.with_unreserved:
             from dcos_commons_amd.specification.specs import VolumeType
 
             def vol(v):
@@ -556,26 +570,89 @@ class _Sim:
 
 
 @dataclass
+class TaskConfig:
+    pod_type: str
+    task_name: str
+    config_name: str
+    content: str
+
+
+@dataclass
 class ServiceTestResult:
     persister: object
     cluster_state: ClusterState
     scheduler: object
     sim: _Sim
+    service_spec: object = None
+    raw_service_spec: object = None
+    scheduler_environment: Dict[str, str] = field(default_factory=dict)
+    task_configs: List[TaskConfig] = field(default_factory=list)
+
+    def get_task_config(self, pod_type: str, task_name: str, config_name: str) -> str:
+        for c in self.task_configs:
+            if (c.pod_type, c.task_name, c.config_name) == (pod_type, task_name, config_name):
+                return c.content
+        raise KeyError(f"no config {config_name} for {pod_type}/{task_name}: "
+                       f"{[(c.pod_type, c.task_name, c.config_name) for c in self.task_configs]}")
+
+
+# Sandbox variables Mesos provides to every task (ServiceTestRunner.DCOS_TASK_ENVVARS)
+DCOS_TASK_ENVVARS = {"MESOS_SANDBOX": "/path/to/mesos/sandbox", "MESOS_CONTAINER_IP": "999.987.654.321",
+                     "STATSD_UDP_HOST": "999.123.456.789", "STATSD_UDP_PORT": "99999"}
 
 
 class ServiceTestRunner:
     """Builds a scheduler from a YAML spec (or a ServiceSpec) and plays ticks against it."""
 
-    def __init__(self, spec_path: Optional[str] = None, spec=None, raw=None):
+    def __init__(self, spec_path: Optional[str] = None, spec=None, raw=None, universe_dir: Optional[str] = None):
         self.spec_path = spec_path
         self.spec = spec
         self.raw = raw
+        self.universe_dir = universe_dir
         self.env: Dict[str, str] = {}
         self.scheduler_env: Dict[str, str] = {}
+        self.options: Dict[str, str] = {}
+        self.build_params: Dict[str, str] = {}
+        self.pod_env: Dict[str, Dict[str, str]] = {}
+        self.validators: List = []
+        self.recovery_factory = None
         self.persister = None
         self.template_dir: Optional[str] = None
         self.customize: Optional[Callable[[SchedulerBuilder], None]] = None
         self.reader = None
+
+    @staticmethod
+    def for_framework(name: str, spec_file: str = "svc.yml") -> "ServiceTestRunner":
+        """Spec + Universe package of ``frameworks/<name>`` (the reference's default runner layout)."""
+        root = os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))),
+                            "frameworks", name)
+        return ServiceTestRunner(os.path.join(root, "specs", spec_file), universe_dir=os.path.join(root, "universe"))
+
+    def set_options(self, *key_vals, **options) -> "ServiceTestRunner":
+        """Universe package options, e.g. ``set_options("service.user", "foo")``."""
+        if len(key_vals) % 2:
+            raise ValueError("expected key/value pairs")
+        self.options.update({key_vals[i]: str(key_vals[i + 1]) for i in range(0, len(key_vals), 2)})
+        self.options.update({k: str(v) for k, v in options.items()})
+        return self
+
+    def set_build_template_params(self, **params) -> "ServiceTestRunner":
+        self.build_params.update({k: str(v) for k, v in params.items()})
+        return self
+
+    def set_pod_env(self, pod_type: str, env: Optional[Dict[str, str]] = None, **kw) -> "ServiceTestRunner":
+        """Task env for rendering ``pod_type``'s config templates (values Main would inject)."""
+        d = self.pod_env.setdefault(pod_type, {})
+        d.update({k: str(v) for k, v in dict(env or {}, **kw).items()})
+        return self
+
+    def set_custom_validators(self, validators) -> "ServiceTestRunner":
+        self.validators = list(validators)
+        return self
+
+    def set_recovery_manager_factory(self, factory) -> "ServiceTestRunner":
+        self.recovery_factory = factory
+        return self
 
     def set_env(self, env: Dict[str, str]) -> "ServiceTestRunner":
         self.env.update({k: str(v) for k, v in env.items()})
@@ -602,16 +679,32 @@ class ServiceTestRunner:
         self.customize = fn
         return self
 
+    def scheduler_environment(self) -> Dict[str, str]:
+        env: Dict[str, str] = {}
+        if self.universe_dir is not None:
+            from dcos_commons_amd.testing.cosmos import render_scheduler_environment
+
+            env.update(render_scheduler_environment(self.universe_dir, self.options, self.build_params))
+        env.update(self.env)
+        env.update(self.scheduler_env)
+        return env
+
     def _build(self):
-        cfg_env = {"PORT_API": "0", "SDK_EVENT_DRIVEN": "false", "SDK_OFFER_HOLD_S": "0"}
+        sched_env = self.scheduler_environment()
+        cfg_env = dict(sched_env) if self.universe_dir is not None else {}
+        cfg_env.update({"PORT_API": "0", "SDK_EVENT_DRIVEN": "false", "SDK_OFFER_HOLD_S": "0"})
         cfg_env.update(self.scheduler_env)
         cfg = SchedulerConfig.for_testing(**cfg_env)
         raw = self.raw
         spec = self.spec
+        render_env = sched_env if self.universe_dir is not None else self.env
         if spec is None:
-            raw = RawServiceSpec.new_builder(self.spec_path).set_env(self.env).build()
+            rb = RawServiceSpec.new_builder(self.spec_path).set_env(render_env)
+            if self.universe_dir is not None:
+                rb.enable_strict_rendering()
+            raw = rb.build()
             gen = ServiceSpecGenerator(raw, cfg, self.template_dir or os.path.dirname(os.path.abspath(self.spec_path)),
-                                       self.env)
+                                       render_env)
             if self.reader is not None:
                 gen.reader = self.reader
             spec = gen.build()
@@ -619,14 +712,43 @@ class ServiceTestRunner:
         builder = SchedulerBuilder(spec, cfg, persister)
         if raw is not None:
             builder.set_plans_from(raw)
+        if self.validators:
+            builder.set_custom_config_validators(self.validators)
+        if self.recovery_factory is not None:
+            builder.set_recovery_manager_factory(self.recovery_factory)
         if self.customize is not None:
             self.customize(builder)
+        self._last = (raw, sched_env)
         return cfg, spec, persister, builder
 
-    def run(self, ticks: Iterable[SimulationTick]) -> ServiceTestResult:
+    def _task_configs(self, spec, cfg) -> List[TaskConfig]:
+        """Renders every config template of pod index 0 strictly (reference Test 4)."""
+        from dcos_commons_amd.offer.evaluate.pod_info_builder import get_task_environment
+        from dcos_commons_amd.specification.specs import PodInstance, PortSpec
+        from dcos_commons_amd.specification.yaml.template_utils import render_mustache_throw_if_missing
+
+        out: List[TaskConfig] = []
+        rng = random.Random(0)
+        for pod in spec.pods:
+            pi = PodInstance(pod, 0)
+            for task in pod.tasks:
+                env = get_task_environment(spec.name, pi, task, cfg)
+                env.update(DCOS_TASK_ENVVARS)
+                for r in task.resource_set.resources:
+                    if isinstance(r, PortSpec) and r.env_key:
+                        env[r.env_key] = str(r.port or rng.randrange(32768, 61000))
+                env.update(self.pod_env.get(pod.type, {}))
+                for c in task.config_files:
+                    content = render_mustache_throw_if_missing(
+                        f"pod={pod.type} task={task.name} config={c.name}", c.template_content, env)
+                    out.append(TaskConfig(pod.type, task.name, c.name, content))
+        return out
+
+    def run(self, ticks: Iterable[SimulationTick] = ()) -> ServiceTestResult:
         ProcessExit.set_test_mode(True)
         task_killer.reset(executor_enabled=False)
         cfg, spec, persister, builder = self._build()
+        task_configs = self._task_configs(spec, cfg) if self.universe_dir is not None or self.pod_env else []
         scheduler = builder.build()
         fc = FrameworkConfig.from_service_spec(spec)
         roles = set(fc.pre_reserved_roles) | {fc.role}
@@ -647,4 +769,5 @@ class ServiceTestRunner:
             except AssertionError as e:
                 raise AssertionError(f"tick {i} ({tick.description}) failed: {e}") from e
         task_killer.reset(executor_enabled=True)
-        return ServiceTestResult(persister, state, scheduler, sim)
+        raw, sched_env = self._last
+        return ServiceTestResult(persister, state, scheduler, sim, spec, raw, sched_env, task_configs)

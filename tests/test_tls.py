@@ -269,5 +269,7 @@ def test_tls_requires_service_account():
     spec, _, _ = _pod("tls.yml", TLS_ENV, "artifacts")
     errs = TLSRequiresServiceAccount(SchedulerConfig.for_testing()).validate(None, spec)
     assert errs and "service account" in str(errs[0])
-    ok = SchedulerConfig.for_testing(DCOS_SERVICE_ACCOUNT_CREDENTIAL="{}")
+    bad = SchedulerConfig.for_testing(DCOS_SERVICE_ACCOUNT_CREDENTIAL="{}")  # no uid / private_key
+    assert TLSRequiresServiceAccount(bad).validate(None, spec)
+    ok = SchedulerConfig.for_testing(DCOS_SERVICE_ACCOUNT_CREDENTIAL='{"uid": "sa", "private_key": "k"}')
     assert TLSRequiresServiceAccount(ok).validate(None, spec) == []
