@@ -4,6 +4,9 @@
 // tree renderers of cli/queries/{plan,pod}.go. Talks to the scheduler's REST API directly over
 // HTTP/1.1 (no DC/OS cluster configuration needed): --url (or SDK_SCHEDULER_URL) is the scheduler
 // base URL; --service selects a service of a multi-service scheduler (/v1/service/<name>/...).
+#include <sys/wait.h>
+#include <unistd.h>
+
 #include <cstdlib>
 #include <iostream>
 #include <map>
@@ -135,7 +138,52 @@ void usage() {
       "  debug config list|show ID|target|target_id\n"
       "  debug state framework_id|properties|property NAME|refresh_cache\n"
       "  debug pod pause|resume POD [-t TASK]...\n"
-      "  describe | update status | health | metrics\n";
+      "  describe | update status | health | metrics\n"
+      "  hdfs <hdfs args...>   (hdfs services: runs bin/hdfs on name-0-node via `dcos task exec`)\n";
+}
+
+// -- framework plugins (reference: frameworks/hdfs/cli/dcos-hdfs/main.go) --------------------
+
+// Index of `target` if it is the first non-flag argument, else -1: everything after it belongs to
+// the plugin, including flags the SDK parser would otherwise consume (`hdfs dfs -ls /`).
+int first_argument_index(const std::string& target, const std::vector<std::string>& args) {
+  for (size_t i = 0; i < args.size(); ++i) {
+    if (args[i].rfind("-", 0) == 0) continue;
+    return args[i] == target ? static_cast<int>(i) : -1;
+  }
+  return -1;
+}
+
+std::string shell_join(const std::vector<std::string>& args) {
+  std::string out;
+  for (const auto& a : args) out += (out.empty() ? "" : " ") + a;
+  return out;
+}
+
+// Builds `dcos task exec name-0-node bash -c "<hdfs command>"` and runs it as a child process
+// (SDK_CLI_DRY_RUN=1 prints it instead). Returns the child's exit status.
+int hdfs_plugin(const std::vector<std::string>& hdfs_args) {
+  std::vector<std::string> cmd = {"dcos", "task", "exec", "name-0-node", "bash", "-c",
+                                  "export JAVA_HOME=$(ls -d $MESOS_SANDBOX/jdk*/); $HDFS_VERSION/bin/hdfs " +
+                                      shell_join(hdfs_args)};
+  if (const char* dry = std::getenv("SDK_CLI_DRY_RUN"); dry != nullptr && std::string(dry) == "1") {
+    for (size_t i = 0; i < cmd.size(); ++i) std::cout << (i ? "\x1f" : "") << cmd[i];
+    std::cout << std::endl;
+    return 0;
+  }
+  pid_t pid = fork();
+  if (pid < 0) die("fork failed");
+  if (pid == 0) {
+    std::vector<char*> argv;
+    for (auto& a : cmd) argv.push_back(a.data());
+    argv.push_back(nullptr);
+    execvp(argv[0], argv.data());
+    std::cerr << "Failed to run '" << cmd[0] << "': is the DC/OS CLI installed?" << std::endl;
+    _exit(127);
+  }
+  int status = 0;
+  waitpid(pid, &status, 0);
+  return WIFEXITED(status) ? WEXITSTATUS(status) : 1;
 }
 
 int plan_cmd(Ctx& c, const std::vector<std::string>& a) {
@@ -244,6 +292,21 @@ int main(int argc, char** argv) {
   std::string url = std::getenv("SDK_SCHEDULER_URL") ? std::getenv("SDK_SCHEDULER_URL") : "http://127.0.0.1:8080";
   if (const char* tok = std::getenv("DCOS_AUTH_TOKEN")) c.headers["Authorization"] = std::string("token=") + tok;
   std::vector<std::string> a;
+  std::vector<std::string> raw(argv + 1, argv + argc);
+  // flags of the SDK parser take a value: skip it when looking for the plugin section
+  std::vector<std::string> scan;
+  for (size_t i = 0; i < raw.size(); ++i) {
+    if ((raw[i] == "--url" || raw[i] == "--service" || raw[i] == "--name") && i + 1 < raw.size()) {
+      scan.push_back(raw[i]);
+      scan.push_back("-" + raw[++i]);
+    } else {
+      scan.push_back(raw[i]);
+    }
+  }
+  int plugin_at = first_argument_index("hdfs", scan);
+  if (plugin_at >= 0) {
+    argc = plugin_at + 1;  // the SDK parser sees only what precedes the plugin section
+  }
   for (int i = 1; i < argc; ++i) {
     std::string s = argv[i];
     if (s == "--url" && i + 1 < argc) url = argv[++i];
@@ -259,6 +322,7 @@ int main(int argc, char** argv) {
   } catch (const std::exception& e) {
     die(e.what());
   }
+  if (plugin_at >= 0) return hdfs_plugin(std::vector<std::string>(raw.begin() + plugin_at + 1, raw.end()));
   if (a.empty()) {
     usage();
     return 1;

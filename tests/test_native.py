@@ -138,3 +138,21 @@ def test_amd_gpu_probe_binary():
     assert r.returncode == 0, r.stdout + r.stderr
     rep = json.loads(r.stdout)
     assert rep["mfma_tflops"] > 500 and rep["hbm_copy_gbps"] > 2000
+
+
+def test_cli_hdfs_plugin_argument_split(tools):
+    """frameworks/hdfs/cli: everything after a leading `hdfs` section goes to bin/hdfs (main_test.go)."""
+    env = dict(os.environ, SDK_CLI_DRY_RUN="1")
+
+    def run(*args):
+        r = subprocess.run([tools["sdk-cli"], *args], capture_output=True, text=True, timeout=30, env=env)
+        return r.returncode, r.stdout.strip().split("\x1f")
+
+    rc, cmd = run("hdfs", "dfs", "-ls", "/")
+    assert rc == 0 and cmd[:6] == ["dcos", "task", "exec", "name-0-node", "bash", "-c"]
+    assert cmd[6].endswith("bin/hdfs dfs -ls /")
+    rc, cmd = run("--service", "hdfs", "--json", "hdfs", "dfsadmin", "-report", "--help")
+    assert rc == 0 and cmd[6].endswith("bin/hdfs dfsadmin -report --help")  # plugin flags are not parsed
+    r = subprocess.run([tools["sdk-cli"], "--url", "http://127.0.0.1:9", "plan", "hdfs"], capture_output=True,
+                       text=True, timeout=30, env=env)
+    assert "dcos" not in r.stdout  # `hdfs` is not the first argument: regular SDK section
