@@ -178,6 +178,60 @@ class Send(SimulationTick):
         return Send(fn, f"{method} {path}")
 
     @staticmethod
+    def drive_plan(plan: str = "deploy", max_rounds: int = 40, pods: Optional[List[str]] = None) -> "Send":
+        """Plays the cluster until ``plan`` is COMPLETE: each round offers fresh resources for every pod
+        type (new host each time) plus reoffers of every launched pod instance, answers each new
+        launch with RUNNING (+ readiness passed) or FINISHED for FINISH/ONCE goals, and issues a plan
+        ``continue`` when a round makes no progress (canary strategies wait for the operator)."""
+        def fn(sim):
+            from dcos_commons_amd.specification.specs import GoalState
+
+            answered = set()
+            hosts = iter(range(10 ** 6))
+            stalled = 0
+            for _ in range(max_rounds):
+                p = sim.scheduler.get_plan(plan)
+                if p is None:
+                    raise AssertionError(f"no plan {plan}")
+                if p.get_status() == Status.COMPLETE:
+                    return
+                before = len(answered)
+                for pod in sim.state.spec.pods:
+                    if pods is not None and pod.type not in pods:
+                        continue
+                    SendOffer(pod.type).set_hostname(f"auto-{next(hosts)}").build().send(sim)
+                    for i in range(pod.count):
+                        if sim.state.accepts_for_pod(f"{pod.type}-{i}"):
+                            (SendOffer(pod.type).set_pod_index_to_reoffer(i).add_unreserved_resources()
+                             .set_hostname(f"auto-{next(hosts)}").build().send(sim))
+                for a in list(sim.driver.accepts):
+                    for t in a.launched_tasks():
+                        if t.task_id.value in answered:
+                            continue
+                        answered.add(t.task_id.value)
+                        goal = _task_goal(sim.state.spec, t.name)
+                        if goal in (GoalState.FINISH, GoalState.ONCE):
+                            SendTaskStatus(t.name, P.TASK_FINISHED).set_task_id(t.task_id.value).send(sim)
+                        else:
+                            (SendTaskStatus(t.name, P.TASK_RUNNING).set_task_id(t.task_id.value)
+                             .set_readiness_check_exit_code(0).send(sim))
+                if len(answered) == before:
+                    stalled += 1
+                    sim.state.router.post(f"/v1/plans/{plan}/continue")
+                    for ph in p.get_children():
+                        if ph.get_status() in (Status.WAITING, Status.PENDING) or ph.is_interrupted():
+                            sim.state.router.post(f"/v1/plans/{plan}/continue?phase={ph.get_name()}")
+                    if stalled > 5:
+                        break
+                else:
+                    stalled = 0
+            p = sim.scheduler.get_plan(plan)
+            raise AssertionError(f"plan {plan} is {p.get_status()} after {max_rounds} rounds: "
+                                 + "; ".join(f"{ph.get_name()}={[(s.get_name(), str(s.get_status())) for s in ph.get_children()]}"
+                                             for ph in p.get_children()))
+        return Send(fn, f"drive plan {plan} to completion")
+
+    @staticmethod
     def empty_offers() -> "Send":
         return Send(lambda sim: sim.framework.resource_offers(sim.driver, []), "Nudge offer processing")
 
@@ -280,11 +334,22 @@ class SendOffer(Send):
                 return self._unreserved("disk", v.value, mount)
             for v in pod.volumes:
                 o.resources.add().CopyFrom(vol(v))
+            from dcos_commons_amd.specification.specs import PortSpec
+
+            dynamic_ports = False
             for t in pod.tasks:
                 for r in t.resource_set.resources:
+                    if isinstance(r, PortSpec) and r.port == 0:
+                        # agents offer port *ranges*: dynamic ports are claimed from them
+                        dynamic_ports = True
+                        for rg in r.ranges:
+                            o.resources.add().CopyFrom(self._unreserved("ports", _ranges(rg.begin, rg.end)))
+                        continue
                     o.resources.add().CopyFrom(self._unreserved(r.name, r.value))
                 for v in t.resource_set.volumes:
                     o.resources.add().CopyFrom(vol(v))
+            if dynamic_ports:
+                o.resources.add().CopyFrom(self._unreserved("ports", _ranges(10000, 10999)))
             for name, value in sim.cfg.executor_resources().items():
                 o.resources.add().CopyFrom(self._unreserved(name, value))
         o.resources.extend(self.extra)
@@ -298,6 +363,28 @@ class SendOffer(Send):
         offers = [self._offer(sim) for _ in range(self.count)]
         sim.state.sent_offers.extend(offers)
         sim.framework.resource_offers(sim.driver, offers)
+
+
+def _task_goal(spec, task_name: str):
+    """Goal of the TaskSpec behind a ``<pod>-<index>-<task>`` instance name."""
+    for pod in spec.pods:
+        prefix = pod.type + "-"
+        if not task_name.startswith(prefix):
+            continue
+        rest = task_name[len(prefix):]
+        idx, _, name = rest.partition("-")
+        if not idx.isdigit():
+            continue
+        for t in pod.tasks:
+            if t.name == name:
+                return t.goal
+    return None
+
+
+def _ranges(begin: int, end: int) -> P.Value:
+    val = P.Value(type=P.Value.RANGES)
+    val.ranges.range.add(begin=begin, end=end)
+    return val
 
 
 def _scalar(v: float) -> P.Value:
@@ -620,6 +707,7 @@ class ServiceTestRunner:
         self.template_dir: Optional[str] = None
         self.customize: Optional[Callable[[SchedulerBuilder], None]] = None
         self.reader = None
+        self.prior_accepts: List = []
 
     @staticmethod
     def for_framework(name: str, spec_file: str = "svc.yml") -> "ServiceTestRunner":
@@ -662,9 +750,15 @@ class ServiceTestRunner:
         self.scheduler_env.update({k: str(v) for k, v in env.items()})
         return self
 
-    def set_state(self, persister) -> "ServiceTestRunner":
-        """Resume from a previous run's persister (scheduler restart / config update tests)."""
-        self.persister = persister
+    def set_state(self, previous) -> "ServiceTestRunner":
+        """Resume from a previous run (scheduler restart / config update tests): a persister, or a
+        ``ServiceTestResult`` whose cluster state (prior accepts/reservations) is carried over too,
+        like ``ClusterState.withUpdatedConfig`` in the reference runner."""
+        if isinstance(previous, ServiceTestResult):
+            self.persister = previous.persister
+            self.prior_accepts = list(previous.sim.driver.accepts)
+        else:
+            self.persister = previous
         return self
 
     def set_config_template_dir(self, path: str) -> "ServiceTestRunner":
@@ -755,6 +849,7 @@ class ServiceTestRunner:
         framework = FrameworkScheduler(roles, cfg, persister, FrameworkStore(persister), scheduler).disable_threading()
         framework.set_api_server_started()
         driver = RecordingDriver()
+        driver.accepts.extend(self.prior_accepts)
         router = Router(scheduler.get_http_endpoints())
         state = ClusterState(spec, driver, router)
         sim = _Sim(framework, scheduler, driver, state, persister, cfg, getattr(scheduler, "namespace", None))
