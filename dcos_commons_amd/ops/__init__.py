@@ -38,6 +38,8 @@ def _bind(lib: ctypes.CDLL) -> None:
     lib.amdprobe_version.restype = i
     lib.amdprobe_gemm_bf16_nt.argtypes = [vp, vp, vp, i, i, i, vp]
     lib.amdprobe_gemm_bf16_nt.restype = i
+    lib.amdprobe_gemm_bf16_nt_variant.argtypes = [vp, vp, vp, i, i, i, i, vp]
+    lib.amdprobe_gemm_bf16_nt_variant.restype = i
     lib.amdprobe_mfma_peak.argtypes = [vp, i, i, f, vp]
     lib.amdprobe_mfma_peak.restype = i
     lib.amdprobe_mfma_peak_flops.argtypes = [i, i]
@@ -78,8 +80,14 @@ def _check(rc: int, what: str) -> None:
         raise ProbeError(f"{what}: HIP error {rc}")
 
 
-def gemm_bf16_nt(a, bt, out=None):
-    """``a[M,K] @ bt[N,K]^T`` in fp32 on the MFMA tile kernel (M, N % 128 == 0, K % 64 == 0)."""
+GEMM_VARIANTS = {"auto": 0, "tile128": 1, "glds256": 2}
+
+
+def gemm_bf16_nt(a, bt, out=None, variant: str = "auto"):
+    """``a[M,K] @ bt[N,K]^T`` in fp32 on an MFMA kernel (M, N % 128 == 0, K % 64 == 0).
+
+    ``auto`` runs the 256x256 LDS-DMA pipelined kernel when M, N % 256 == 0 and K % 128 == 0 and
+    the 128x128 register-staged kernel otherwise; ``tile128`` / ``glds256`` force one."""
     import torch
 
     if a.dtype != torch.bfloat16 or bt.dtype != torch.bfloat16:
@@ -93,8 +101,10 @@ def gemm_bf16_nt(a, bt, out=None):
     a, bt = a.contiguous(), bt.contiguous()
     if out is None:
         out = torch.empty((m, n), dtype=torch.float32, device=a.device)
-    _check(lib().amdprobe_gemm_bf16_nt(a.data_ptr(), bt.data_ptr(), out.data_ptr(), m, n, k, _stream(a.device)),
-           "gemm_bf16_nt")
+    if variant not in GEMM_VARIANTS:
+        raise ProbeError(f"unknown GEMM variant {variant!r}: {sorted(GEMM_VARIANTS)}")
+    _check(lib().amdprobe_gemm_bf16_nt_variant(a.data_ptr(), bt.data_ptr(), out.data_ptr(), m, n, k,
+                                               GEMM_VARIANTS[variant], _stream(a.device)), "gemm_bf16_nt")
     return out
 
 

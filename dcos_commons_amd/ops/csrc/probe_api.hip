@@ -14,14 +14,31 @@ static bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 
 
 AMDPROBE_EXPORT int amdprobe_version() { return 1; }
 
-AMDPROBE_EXPORT int amdprobe_gemm_bf16_nt(const void* A, const void* Bt, float* C, int M, int N, int K,
-                                          void* stream) {
-  if (M <= 0 || N <= 0 || K <= 0 || M % BM || N % BN || K % BK) return ERR_SHAPE;
+// variant: 0 = pick (256x256 glds pipeline when the shape allows, else 128x128),
+//          1 = 128x128 register-staged, 2 = 256x256 glds pipeline (M, N % 256 == 0, K % 128 == 0)
+AMDPROBE_EXPORT int amdprobe_gemm_bf16_nt_variant(const void* A, const void* Bt, float* C, int M, int N, int K,
+                                                  int variant, void* stream) {
+  if (M <= 0 || N <= 0 || K <= 0) return ERR_SHAPE;
   if (!aligned16(A) || !aligned16(Bt) || !aligned16(C)) return ERR_ALIGN;
+  const bool big_ok = M % big::BM == 0 && N % big::BN == 0 && K % (2 * big::BK) == 0;
+  if (variant == 0) variant = big_ok ? 2 : 1;
+  if (variant == 2) {
+    if (!big_ok) return ERR_SHAPE;
+    const int nwg = (M / big::BM) * (N / big::BN);
+    hipLaunchKernelGGL(gemm_bf16_nt_256_kernel, dim3(nwg), dim3(big::THREADS), 0, (hipStream_t)stream,
+                       (const __bf16*)A, (const __bf16*)Bt, C, M, N, K);
+    return (int)hipGetLastError();
+  }
+  if (variant != 1 || M % BM || N % BN || K % BK) return ERR_SHAPE;
   const int nwg = (M / BM) * (N / BN);
   hipLaunchKernelGGL(gemm_bf16_nt_kernel, dim3(nwg), dim3(GEMM_THREADS), 0, (hipStream_t)stream,
                      (const __bf16*)A, (const __bf16*)Bt, C, M, N, K);
   return (int)hipGetLastError();
+}
+
+AMDPROBE_EXPORT int amdprobe_gemm_bf16_nt(const void* A, const void* Bt, float* C, int M, int N, int K,
+                                          void* stream) {
+  return amdprobe_gemm_bf16_nt_variant(A, Bt, C, M, N, K, 0, stream);
 }
 
 AMDPROBE_EXPORT int amdprobe_mfma_peak(float* out, int blocks, int iters, float seed, void* stream) {

@@ -41,14 +41,27 @@ __device__ __forceinline__ int xcd_remap(int orig, int nwg) {
   return base + (orig >> 3);
 }
 
+// Grouped tile order: consecutive tile ids walk GM-row bands column by column, so the ~32 tiles
+// one XCD has in flight form a GM x (32/GM) block that shares GM A-panels and 32/GM B-panels in
+// that XCD's L2 instead of 1 A-panel and 32 B-panels (row-major order). Bijective; the last band
+// may be shorter than GM.
+__device__ __forceinline__ void grouped_tile(int tile, int tiles_m, int tiles_n, int gm, int& tm, int& tn) {
+  const int band = tile / (gm * tiles_n);
+  const int first = band * gm;
+  const int rows = min(gm, tiles_m - first);
+  const int in = tile - band * gm * tiles_n;
+  tm = first + in % rows;
+  tn = in / rows;
+}
+
 __global__ __launch_bounds__(GEMM_THREADS, 2)
 void gemm_bf16_nt_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt,
                          float* __restrict__ C, int M, int N, int K) {
   __shared__ __attribute__((aligned(16))) __bf16 lds[2 * 2 * TILE_ELEMS];  // [buf][A|B][row][k]
   const int tiles_n = N / BN;
   const int nwg = (M / BM) * tiles_n;
-  const int tile = xcd_remap(blockIdx.x, nwg);
-  const int tm = tile / tiles_n, tn = tile % tiles_n;
+  int tm, tn;
+  grouped_tile(xcd_remap(blockIdx.x, nwg), M / BM, tiles_n, 8, tm, tn);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wr = wave >> 1, wc = wave & 1;
 
@@ -139,6 +152,202 @@ void gemm_bf16_nt_kernel(const __bf16* __restrict__ A, const __bf16* __restrict_
         const int col = wc * 64 + n * 16 + (lane & 15);
         Cblk[(size_t)row * N + col] = acc[m][n][j];
       }
+}
+
+// ---------------------------------------------------------------------------------------
+// bf16 GEMM, 256x256 block tile, LDS-DMA staged 8-phase pipeline (the fast path).
+//
+// 512 threads = 8 waves as 2 (M) x 4 (N); wave (wr, wc) owns a 128x64 output: rows
+// {wr*64 + [0,64)} u {128 + wr*64 + [0,64)}, cols {wc*32 + [0,32)} u {128 + wc*32 + [0,32)},
+// i.e. 8 x 4 MFMA 16x16 tiles (128 accumulator VGPRs). Interleaving the two halves means every
+// wave's first A/B fragments sit in the "lo" half-tiles: a K-tile (256x64 of A and of B) is
+// staged as four 16 KiB half-tiles in consumption order
+//     h0 = A rows 0-127, h1 = B rows 0-127, h2 = B rows 128-255, h3 = A rows 128-255
+// and read in four phases per K-tile, one C quadrant (4m x 2n tiles x K=64 = 16 MFMA) each:
+//     ph0: A[m0-3] + B[n0-1] -> MFMA   ph1: B[n2-3] -> MFMA   ph2: A[m4-7] -> MFMA   ph3: MFMA
+// (B[n0-1] stays in registers for ph3). Two K-tiles per loop iteration (8 phases, two LDS
+// buffers of 64 KiB). Every phase issues ONE half-tile of global_load_lds_dwordx4 (2 per
+// thread) six half-tiles ahead; the LDS-DMA stays in flight across the raw s_barriers and is
+// retired by counted `s_waitcnt vmcnt(8)` (never 0 in steady state) one phase before it is read.
+// The two wave groups (wr = 0/1, one wave of each per SIMD) run one barrier apart, so LDS reads
+// of one group overlap MFMA of the other; restaging therefore waits >= 2 phases after a buffer's
+// last read (see the schedule comment in the kernel).
+//
+// LDS image: 128 B rows, 16-B chunk c of row r stored at chunk c ^ ((r >> 1) & 7). LDS-DMA writes
+// lane-linearly, so the permutation is applied to the per-lane global SOURCE address and undone
+// on the ds_read address; for the 16x16x32 fragment reads this is conflict-free in all four
+// ds_read_b128 lane groups.
+// ---------------------------------------------------------------------------------------
+namespace big {
+constexpr int BM = 256, BN = 256, BK = 64, THREADS = 512;
+constexpr int HALF_BYTES = 128 * BK * 2;       // 16 KiB
+constexpr int TILE_BYTES = 4 * HALF_BYTES;     // one K-tile (A and B)
+constexpr int LDS_BYTES = 2 * TILE_BYTES;      // 128 KiB, double buffered
+}  // namespace big
+
+typedef __attribute__((address_space(3))) void lds_void;
+typedef const __attribute__((address_space(1))) void gbl_void;
+
+__device__ __forceinline__ void glds16(const void* gsrc, char* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds((gbl_void*)gsrc, (lds_void*)lds_wave_base, 16, 0, 0);
+}
+
+__global__ __launch_bounds__(big::THREADS, 1)
+void gemm_bf16_nt_256_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt,
+                             float* __restrict__ C, int M, int N, int K) {
+  constexpr int BM = big::BM, BN = big::BN, BK = big::BK;
+  constexpr int HALF_BYTES = big::HALF_BYTES, TILE_BYTES = big::TILE_BYTES, LDS_BYTES = big::LDS_BYTES;
+  __shared__ __attribute__((aligned(1024))) char smem[LDS_BYTES];
+  const int tiles_n = N / BN;
+  const int nwg = (M / BM) * tiles_n;
+  int tm, tn;
+  grouped_tile(xcd_remap(blockIdx.x, nwg), M / BM, tiles_n, 8, tm, tn);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 2, wc = wave & 3;
+
+  const __bf16* Ablk = A + (size_t)tm * BM * K;
+  const __bf16* Bblk = Bt + (size_t)tn * BN * K;
+  // staging: this lane's two 16-B pieces of a half-tile (loop invariant element offsets)
+  size_t soff[2];
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int p = q * 512 + wave * 64 + lane;      // 16-B slot in the half-tile image
+    const int row = p >> 3, chunk = (p & 7) ^ ((row >> 1) & 7);
+    soff[q] = (size_t)row * K + chunk * 8;
+  }
+  const __bf16* hsrc[4] = {Ablk, Bblk, Bblk + (size_t)128 * K, Ablk + (size_t)128 * K};
+  char* const wave_dst = smem + wave * 1024;
+  auto stage = [&](int t, int h) {
+    const __bf16* src = hsrc[h] + (size_t)t * BK;
+    char* dst = wave_dst + (t & 1) * TILE_BYTES + h * HALF_BYTES;
+    glds16(src + soff[0], dst);
+    glds16(src + soff[1], dst + 8192);
+  };
+  // fragment reads: row (lane & 15) of a 16-row group, logical chunk ks*4 + (lane >> 4)
+  const int sw = (lane >> 1) & 7;
+  const int cb0 = (((lane >> 4)) ^ sw) << 4, cb1 = ((4 + (lane >> 4)) ^ sw) << 4;
+  const int rA = (wr * 64 + (lane & 15)) * 128;   // within an A half-tile
+  const int rB = (wc * 32 + (lane & 15)) * 128;   // within a B half-tile
+
+  floatx4 acc[8][4];
+#pragma unroll
+  for (int m = 0; m < 8; ++m)
+#pragma unroll
+    for (int n = 0; n < 4; ++n) acc[m][n] = floatx4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 af[4][2], b0[2][2], b1[2][2];
+
+  // Staging stream: half-tile s = 4*t + h (h: 0 A-lo, 1 B-lo, 2 B-hi, 3 A-hi) is issued in phase
+  // g = s - 6 (global phase g = 4*t + q reads K-tile t's quadrant q). A half-tile is first/last
+  // read in one phase (A-lo, B-lo at q=0, B-hi at q=1, A-hi at q=2), so every restage lands >= 2
+  // phases after the previous occupant's read (the staggered-groups WAR rule) and every read
+  // comes >= 5 phases after its issue. Counted waits (before the phase's first barrier) retire
+  // what the NEXT phase reads: q=0 -> B-hi(t), q=1 -> A-hi(t), q=3 -> A-lo/B-lo(t+1); steady
+  // state keeps 4 half-tiles (8 DMA per thread) in flight.
+  const int nt = K / BK, niter = nt / 2;
+  // prologue: half-tiles 0..5, then retire 0 and 1 (K-tile 0's q=0 operands)
+#pragma unroll
+  for (int s = 0; s < 6; ++s) stage(s >> 2, s & 3);
+  asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  // wave-group stagger: group wr == 1 runs one barrier behind group 0 for the whole loop, so on
+  // every SIMD (waves w and w + 4) one wave reads LDS while the other issues MFMA.
+  const bool late = __builtin_amdgcn_readfirstlane(wr) == 1;
+  if (late) __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_s_barrier();
+
+#define READ_A(T, H)                                                                         \
+  _Pragma("unroll") for (int mm = 0; mm < 4; ++mm) {                                         \
+    const char* base = smem + (T) * TILE_BYTES + (H) * HALF_BYTES + rA + mm * 16 * 128;      \
+    af[mm][0] = *reinterpret_cast<const bf16x8*>(base + cb0);                                \
+    af[mm][1] = *reinterpret_cast<const bf16x8*>(base + cb1);                                \
+  }
+#define READ_B(DST, T, H)                                                                    \
+  _Pragma("unroll") for (int nn = 0; nn < 2; ++nn) {                                         \
+    const char* base = smem + (T) * TILE_BYTES + (H) * HALF_BYTES + rB + nn * 16 * 128;      \
+    DST[nn][0] = *reinterpret_cast<const bf16x8*>(base + cb0);                               \
+    DST[nn][1] = *reinterpret_cast<const bf16x8*>(base + cb1);                               \
+  }
+#define MFMA_Q(MB, NB, BREG)                                                                 \
+  __builtin_amdgcn_s_setprio(1);                                                             \
+  _Pragma("unroll") for (int ks = 0; ks < 2; ++ks)                                           \
+  _Pragma("unroll") for (int mm = 0; mm < 4; ++mm)                                           \
+  _Pragma("unroll") for (int nn = 0; nn < 2; ++nn)                                           \
+    acc[(MB) + mm][(NB) + nn] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(                     \
+        af[mm][ks], BREG[nn][ks], acc[(MB) + mm][(NB) + nn], 0, 0, 0);                       \
+  __builtin_amdgcn_s_setprio(0);
+#define SYNC_MFMA(MB, NB, BREG)                                                              \
+  __builtin_amdgcn_s_barrier();                                                              \
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                         \
+  MFMA_Q(MB, NB, BREG)                                                                       \
+  __builtin_amdgcn_s_barrier();
+#define WAITV(N) asm volatile("s_waitcnt vmcnt(" #N ")" ::: "memory");
+
+  for (int it = 0; it < niter; ++it) {
+    const bool last = it == niter - 1;   // K-tiles nt-2 (even) and nt-1 (odd)
+    const int t0 = 2 * it;
+    // ---- K-tile t0, buffer 0 ----  (q=0..3 issue s = 4*t0 + 6 .. 4*t0 + 9)
+    READ_A(0, 0) READ_B(b0, 0, 1)
+    stage(t0 + 1, 2);
+    WAITV(8)                                                      // B-hi(t0)
+    SYNC_MFMA(0, 0, b0)
+    READ_B(b1, 0, 2)
+    stage(t0 + 1, 3);
+    WAITV(8)                                                      // A-hi(t0)
+    SYNC_MFMA(0, 2, b1)
+    READ_A(0, 3)
+    if (!last) stage(t0 + 2, 0);
+    SYNC_MFMA(4, 2, b1)
+    if (!last) {
+      stage(t0 + 2, 1);
+      WAITV(8)                                                    // A-lo, B-lo(t0 + 1)
+    } else {
+      WAITV(4)
+    }
+    SYNC_MFMA(4, 0, b0)
+    // ---- K-tile t0 + 1, buffer 1 ----
+    READ_A(1, 0) READ_B(b0, 1, 1)
+    if (!last) {
+      stage(t0 + 2, 2);
+      WAITV(8)
+    } else {
+      WAITV(2)
+    }
+    SYNC_MFMA(0, 0, b0)
+    READ_B(b1, 1, 2)
+    if (!last) {
+      stage(t0 + 2, 3);
+      WAITV(8)
+    } else {
+      WAITV(0)
+    }
+    SYNC_MFMA(0, 2, b1)
+    READ_A(1, 3)
+    if (!last) stage(t0 + 3, 0);
+    SYNC_MFMA(4, 2, b1)
+    if (!last) {
+      stage(t0 + 3, 1);
+      WAITV(8)                                                    // A-lo, B-lo(t0 + 2)
+    }
+    SYNC_MFMA(4, 0, b0)
+  }
+  if (!late) __builtin_amdgcn_s_barrier();   // balance the stagger barrier
+#undef READ_A
+#undef READ_B
+#undef MFMA_Q
+#undef SYNC_MFMA
+#undef WAITV
+
+  // epilogue: acc[m][n] element j -> row (lane >> 4) * 4 + j, col lane & 15 of its 16x16 tile
+  float* Cblk = C + (size_t)tm * BM * N + (size_t)tn * BN;
+#pragma unroll
+  for (int m = 0; m < 8; ++m) {
+    const int row0 = (m < 4 ? 0 : 128) + wr * 64 + (m & 3) * 16 + (lane >> 4) * 4;
+#pragma unroll
+    for (int n = 0; n < 4; ++n) {
+      const int col = (n < 2 ? 0 : 128) + wc * 32 + (n & 1) * 16 + (lane & 15);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) Cblk[(size_t)(row0 + j) * N + col] = acc[m][n][j];
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------------------

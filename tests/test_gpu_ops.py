@@ -45,12 +45,46 @@ def test_gemm_exact_integer_asymmetric(dev):
     assert torch.equal(c, ref)
 
 
+@pytest.mark.parametrize("m,n,k", [(256, 256, 128), (512, 768, 384), (768, 512, 256), (1024, 1024, 2048),
+                                   (2048, 256, 1152)])
+def test_gemm_glds256_matches_fp32_reference(dev, m, n, k):
+    """256x256 LDS-DMA pipeline: one-iteration (K=128), odd iteration counts, rectangular grids."""
+    from dcos_commons_amd import ops
+
+    g = torch.Generator(device=dev)
+    g.manual_seed(m + 3 * n + 11 * k)
+    a = (torch.rand((m, k), generator=g, device=dev) * 2 - 1).to(torch.bfloat16)
+    bt = (torch.rand((n, k), generator=g, device=dev) * 2 - 1).to(torch.bfloat16)
+    c = ops.gemm_bf16_nt(a, bt, variant="glds256")
+    ref = a.float() @ bt.float().t()
+    torch.cuda.synchronize()
+    rel = (torch.linalg.norm(c - ref) / torch.linalg.norm(ref)).item()
+    assert rel < 1e-5, rel
+    c128 = ops.gemm_bf16_nt(a, bt, variant="tile128")
+    assert torch.allclose(c, c128, rtol=1e-4, atol=1e-3)
+
+
+def test_gemm_glds256_exact_integer_layout(dev):
+    """Exact small-integer products pin every row/column of the interleaved wave decomposition."""
+    from dcos_commons_amd import ops
+
+    m, n, k = 512, 768, 256
+    a = ((torch.arange(m, device=dev).view(m, 1) * 7 + torch.arange(k, device=dev).view(1, k)) % 5 - 2).float()
+    bt = ((torch.arange(n, device=dev).view(n, 1) * 3 + torch.arange(k, device=dev).view(1, k) * 11) % 7 - 3).float()
+    c = ops.gemm_bf16_nt(a.to(torch.bfloat16), bt.to(torch.bfloat16), variant="glds256")
+    assert torch.equal(c, a @ bt.t())
+
+
 def test_gemm_rejects_bad_shapes(dev):
     from dcos_commons_amd import ops
 
     a = torch.zeros((100, 64), device=dev, dtype=torch.bfloat16)
     with pytest.raises(ops.ProbeError):
         ops.gemm_bf16_nt(a, a)
+    b = torch.zeros((256, 64), device=dev, dtype=torch.bfloat16)  # K % 128 != 0
+    with pytest.raises(ops.ProbeError):
+        ops.gemm_bf16_nt(b, b, variant="glds256")
+    assert ops.gemm_bf16_nt(b, b).shape == (256, 256)  # auto falls back to the 128 kernel
 
 
 def test_hbm_copy_and_pattern(dev):
