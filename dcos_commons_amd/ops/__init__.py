@@ -124,7 +124,7 @@ def mfma_peak(device=0, blocks: int = 2048, iters: int = 2048):
     return e0.elapsed_time(e1) / 1e3, lib().amdprobe_mfma_peak_flops(blocks, iters)
 
 
-def hbm_copy(src, dst, blocks: int = 2048):
+def hbm_copy(src, dst, blocks: int = 4096):
     nbytes = src.numel() * src.element_size()
     if dst.numel() * dst.element_size() < nbytes:
         raise ProbeError("hbm_copy destination too small")

@@ -3,10 +3,11 @@
 // Used as the readiness-check command of GPU pods (frameworks/helloworld/specs/gpu.yml): a pod
 // that was given GPUs is only "ready" once the devices pass
 //   --readiness : MFMA bf16 GEMM numerics (vs a host fp64 reference) + HBM address-hash pattern
-//   --full      : additionally MFMA issue rate (TFLOP/s), 4096^3 GEMM rate and HBM copy bandwidth
+//   --full      : additionally MFMA issue rate (TFLOP/s), 8192^3 GEMM rate and HBM copy bandwidth
 // Exit status 0 = healthy, 1 = unhealthy, 2 = usage / HIP error. --json prints one JSON line.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -63,7 +64,18 @@ struct Report {
   bool healthy = false;
 };
 
-double gemm_check(hipStream_t st, int M, int N, int K, uint64_t seed) {
+// Launches the probe GEMM the way the in-process op does: the 256x256 LDS-DMA pipeline when the
+// shape allows (big256 == true), else the 128x128 register-staged kernel.
+void launch_gemm(hipStream_t st, bool big256, const void* a, const void* b, float* c, int M, int N, int K) {
+  if (big256)
+    hipLaunchKernelGGL(gemm_bf16_nt_256_kernel, dim3((M / big::BM) * (N / big::BN)), dim3(big::THREADS), 0, st,
+                       static_cast<const __bf16*>(a), static_cast<const __bf16*>(b), c, M, N, K);
+  else
+    hipLaunchKernelGGL(gemm_bf16_nt_kernel, dim3((M / BM) * (N / BN)), dim3(GEMM_THREADS), 0, st,
+                       static_cast<const __bf16*>(a), static_cast<const __bf16*>(b), c, M, N, K);
+}
+
+double gemm_check(hipStream_t st, bool big256, int M, int N, int K, uint64_t seed) {
   std::vector<uint16_t> a(static_cast<size_t>(M) * K), b(static_cast<size_t>(N) * K);
   Lcg g(seed);
   for (auto& x : a) x = f32_to_bf16(g.next());
@@ -75,8 +87,7 @@ double gemm_check(hipStream_t st, int M, int N, int K, uint64_t seed) {
   HIP_OK(hipMalloc(&dc, static_cast<size_t>(M) * N * 4));
   HIP_OK(hipMemcpyAsync(da, a.data(), a.size() * 2, hipMemcpyHostToDevice, st));
   HIP_OK(hipMemcpyAsync(db, b.data(), b.size() * 2, hipMemcpyHostToDevice, st));
-  hipLaunchKernelGGL(gemm_bf16_nt_kernel, dim3((M / BM) * (N / BN)), dim3(GEMM_THREADS), 0, st,
-                     static_cast<const __bf16*>(da), static_cast<const __bf16*>(db), dc, M, N, K);
+  launch_gemm(st, big256, da, db, dc, M, N, K);
   HIP_OK(hipGetLastError());
   std::vector<float> c(static_cast<size_t>(M) * N);
   HIP_OK(hipMemcpyAsync(c.data(), dc, c.size() * 4, hipMemcpyDeviceToHost, st));
@@ -147,19 +158,19 @@ void perf(hipStream_t st, Report& r) {
   double flops = static_cast<double>(blocks) * 4 * iters * 4 * (32.0 * 32 * 16 * 2);
   r.mfma_tflops = flops / (ms / 1e3) / 1e12;
   HIP_OK(hipFree(out));
-  // GEMM rate
-  const int S = 4096;
+  // GEMM rate: 8192^3 on the 256x256 pipeline (1024 tiles = 4 per CU), operands filled with an
+  // address-hashed bit pattern (constant operands would understate switching power)
+  const int S = 8192;
   void *a, *b;
   float* c;
   HIP_OK(hipMalloc(&a, static_cast<size_t>(S) * S * 2));
   HIP_OK(hipMalloc(&b, static_cast<size_t>(S) * S * 2));
   HIP_OK(hipMalloc(&c, static_cast<size_t>(S) * S * 4));
-  HIP_OK(hipMemsetAsync(a, 0x3c, static_cast<size_t>(S) * S * 2, st));
-  HIP_OK(hipMemsetAsync(b, 0x3c, static_cast<size_t>(S) * S * 2, st));
-  ms = time_ms(st, 5, [&] {
-    hipLaunchKernelGGL(gemm_bf16_nt_kernel, dim3((S / BM) * (S / BN)), dim3(GEMM_THREADS), 0, st,
-                       static_cast<const __bf16*>(a), static_cast<const __bf16*>(b), c, S, S, S);
-  });
+  hipLaunchKernelGGL(bf16_fill_kernel, dim3(2048), dim3(256), 0, st, static_cast<uint4*>(a),
+                     static_cast<size_t>(S) * S / 8, 11u);
+  hipLaunchKernelGGL(bf16_fill_kernel, dim3(2048), dim3(256), 0, st, static_cast<uint4*>(b),
+                     static_cast<size_t>(S) * S / 8, 12u);
+  ms = time_ms(st, 5, [&] { launch_gemm(st, true, a, b, c, S, S, S); });
   r.gemm_tflops = 2.0 * S * S * static_cast<double>(S) / (ms / 1e3) / 1e12;
   HIP_OK(hipFree(a));
   HIP_OK(hipFree(b));
@@ -170,7 +181,7 @@ void perf(hipStream_t st, Report& r) {
   HIP_OK(hipMalloc(&s0, bytes));
   HIP_OK(hipMalloc(&s1, bytes));
   ms = time_ms(st, 5, [&] {
-    hipLaunchKernelGGL(hbm_copy_kernel, dim3(2048), dim3(256), 0, st, static_cast<const uint4*>(s0),
+    hipLaunchKernelGGL(hbm_copy_kernel, dim3(HBM_COPY_BLOCKS), dim3(256), 0, st, static_cast<const uint4*>(s0),
                        static_cast<uint4*>(s1), bytes / 16);
   });
   r.hbm_gbps = 2.0 * bytes / (ms / 1e3) / 1e9;
@@ -219,7 +230,8 @@ int main(int argc, char** argv) {
   Report r;
   r.device = device;
   r.arch = prop.gcnArchName;
-  r.gemm_rel_err = gemm_check(st, 256, 256, 512, 1234 + device);
+  r.gemm_rel_err = std::max(gemm_check(st, false, 256, 256, 512, 1234 + device),
+                            gemm_check(st, true, 512, 256, 512, 4321 + device));
   r.mem_bad_words = mem_check(st, 64u << 20, 77u + device);
   bool ok = r.gemm_rel_err < 1e-3 && r.mem_bad_words == 0;
   if (full) {

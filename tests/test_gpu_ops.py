@@ -87,6 +87,16 @@ def test_gemm_rejects_bad_shapes(dev):
     assert ops.gemm_bf16_nt(b, b).shape == (256, 256)  # auto falls back to the 128 kernel
 
 
+@pytest.mark.parametrize("n,blocks", [(4, 4096), (4 * 1023 + 4, 7), (4 * 1024 * 5, 1), (4 * 300001, 4096)])
+def test_hbm_copy_spans_and_tails(dev, n, blocks):
+    from dcos_commons_amd import ops
+
+    src = torch.randint(-2**31, 2**31 - 1, (n,), device=dev, dtype=torch.int32)
+    dst = torch.zeros(n + 64, device=dev, dtype=torch.int32)
+    ops.hbm_copy(src, dst[:n], blocks=blocks)
+    assert torch.equal(src, dst[:n]) and not dst[n:].any()  # nothing written past the end
+
+
 def test_hbm_copy_and_pattern(dev):
     from dcos_commons_amd import ops
 
