@@ -40,8 +40,9 @@ PROFILES = {
     "mi355x": {},  # framework defaults: event-driven wake-ups, 10 s offer holding, 1 s revive spacing
     # the reference's cadence on the same harness
     "reference": {"SDK_EVENT_DRIVEN": "false", "SDK_OFFER_HOLD_S": "0", "SDK_OFFER_WAIT_S": "5",
-                  "SDK_REVIVE_INTERVAL_S": "5", "SDK_RESERVATION_GC_ALL_OFFERS": "false",
-                  "SDK_FAST_UNSUPPRESS": "false"},
+                  "SDK_REVIVE_INTERVAL_S": "5", "SDK_REVIVE_BURST_INTERVAL_S": "5",
+                  "SDK_RESERVATION_GC_ALL_OFFERS": "false",
+                  "SDK_FAST_UNSUPPRESS": "false", "SDK_MERGE_AGENT_OFFERS": "false"},
 }
 
 

@@ -1,0 +1,233 @@
+"""Framework-level benchmarks for the remaining BASELINE.json configs (the headline helloworld
+deploy/MTTR bench lives in ``deploy_bench``):
+
+* **cassandra, 3 nodes** -- deploy plan COMPLETE wall-clock (serial ``node`` phase plus the ONCE
+  ``init_system_keyspaces`` step), then ``POST /v1/pod/node-<i>/replace`` until the replacement
+  server is RUNNING + ready and the recovery plan is COMPLETE. The recovery phase must come from
+  ``CassandraRecoveryPlanOverrider`` (``-Dcassandra.replace_address=<old ip>`` on the new server's
+  command; reference: frameworks/cassandra/.../CassandraRecoveryPlanOverrider.java:66-101).
+* **hdfs, HA layout** (3 journal, 2 name with zkfc, 3 data) -- deploy plan COMPLETE wall-clock
+  (multi-step phases: ``journal`` bootstrap + node, ``name`` format/bootstrap/zkfc-format + node/zkfc,
+  ``data``), then a configuration change rolled out by a scheduler restart: the ``update`` plan
+  (journal serial -> name ``[[node, zkfc]]`` -> data serial; reference frameworks/hdfs/src/main/dist/
+  svc.yml:566-611) replaces deploy and is timed until COMPLETE with every task relaunched.
+
+Both run the real scheduler (offer loop, plan engine, state store, HTTP API) against the in-process
+Mesos master (``LocalMaster``) with synthetic task payloads: RUNNING tasks start at once, ONCE/FINISH
+tasks exit FINISHED at once and readiness checks pass without their configured delays, so the numbers
+are scheduler cost, not Cassandra/HDFS start-up time. ``profile="reference"`` replays the
+reference's offer cadence (5 s poll, throttled revives; see ``deploy_bench.PROFILES``).
+"""
+from __future__ import annotations
+
+import os
+import time
+from dataclasses import dataclass
+from typing import Dict, List, Optional
+
+from dcos_commons_amd.framework.process_exit import ProcessExit
+from dcos_commons_amd.mesos import protos as P
+from dcos_commons_amd.mesos.local_master import AgentSpec, LocalMaster, LocalSchedulerDriver, TaskBehavior, TaskTiming
+from dcos_commons_amd.offer.taskdata.labels import TaskLabelReader
+from dcos_commons_amd.scheduler.scheduler_config import SchedulerConfig
+from dcos_commons_amd.scheduler.scheduler_runner import SchedulerRunner
+from dcos_commons_amd.state.state_store_utils import get_deployment_was_completed
+from dcos_commons_amd.storage.mem_persister import MemPersister
+
+from .deploy_bench import PROFILES
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+# task-name fragments of the ONCE/FINISH tasks: they exit FINISHED right after RUNNING
+_FINISHING = ("init_system_keyspaces", "-bootstrap", "-format")
+
+
+@dataclass
+class FrameworkCycle:
+    framework: str
+    deploy_s: float
+    second_s: float          # cassandra: replace-node MTTR; hdfs: rolling config update
+    second_name: str
+    tasks: int
+    total_s: float
+
+    def as_dict(self) -> Dict[str, float]:
+        return {"framework": self.framework, "deploy_s": round(self.deploy_s, 6),
+                self.second_name: round(self.second_s, 6), "tasks": self.tasks, "total_s": round(self.total_s, 6)}
+
+
+def _behavior() -> TaskBehavior:
+    finish = TaskTiming(finish_after_s=0.0, honor_check_delays=False)
+    return TaskBehavior(TaskTiming(honor_check_delays=False), overrides={k: finish for k in _FINISHING})
+
+
+def _scheduler_env(framework: str, **extra: str) -> Dict[str, str]:
+    from dcos_commons_amd.testing.cosmos import render_scheduler_environment
+
+    env = render_scheduler_environment(os.path.join(ROOT, "frameworks", framework, "universe"), {}, {})
+    env.update(extra)
+    return env
+
+
+class FrameworkBench:
+    def __init__(self, framework: str, profile: str = "mi355x", allocation_interval_s: float = 1.0,
+                 timeout_s: float = 120.0):
+        if framework not in ("cassandra", "hdfs"):
+            raise ValueError(f"unknown framework {framework!r}")
+        self.framework = framework
+        self.profile = profile
+        self.allocation_interval_s = allocation_interval_s
+        self.timeout_s = timeout_s
+
+    # -- helpers ---------------------------------------------------------------------------
+    def _wait(self, pred, what: str) -> float:
+        t0 = time.perf_counter()
+        while not pred():
+            if time.perf_counter() - t0 > self.timeout_s:
+                raise TimeoutError(f"timed out after {self.timeout_s}s waiting for {what}")
+            time.sleep(0.001)
+        return time.perf_counter() - t0
+
+    def _config(self) -> SchedulerConfig:
+        overrides = dict(PROFILES[self.profile])
+        overrides.update({"PORT_API": "0", "SDK_PERSISTER": "mem"})
+        return SchedulerConfig.for_testing(**overrides)
+
+    def _master(self, agents: int) -> LocalMaster:
+        master = LocalMaster(allocation_interval_s=self.allocation_interval_s, behavior=_behavior())
+        for i in range(agents):
+            master.add_agent(AgentSpec(hostname=f"agent-{i}", cpus=32, mem=262144, disk=2_000_000,
+                                       ports=((1025, 32000),)))  # cassandra/hdfs use fixed ports
+        return master
+
+    def _builder(self, env: Dict[str, str], cfg: SchedulerConfig, persister):
+        spec = os.path.join(ROOT, "frameworks", self.framework, "specs", "svc.yml")
+        if self.framework == "cassandra":
+            from dcos_commons_amd.models import cassandra as m
+        else:
+            from dcos_commons_amd.models import hdfs as m
+        return m.create_scheduler_builder(spec, cfg, env, persister)
+
+    @staticmethod
+    def _ready(state_store, task_name: str, old_task_id: Optional[str]) -> bool:
+        info = state_store.fetch_task(task_name)
+        st = state_store.fetch_status(task_name)
+        if info is None or st is None or st.state != P.TASK_RUNNING:
+            return False
+        if st.task_id.value != info.task_id.value or (old_task_id is not None and st.task_id.value == old_task_id):
+            return False
+        return TaskLabelReader(info).is_readiness_check_succeeded(st)
+
+    def _start(self, master, env, cfg, persister):
+        runner = SchedulerRunner(self._builder(env, cfg, persister),
+                                 driver_factory=lambda s, info: LocalSchedulerDriver(master, s, info))
+        runner.run(block=False)
+        return runner
+
+    # -- cycles ----------------------------------------------------------------------------
+    def run_cycle(self) -> FrameworkCycle:
+        ProcessExit.set_test_mode(True)
+        return self._cassandra() if self.framework == "cassandra" else self._hdfs()
+
+    def _cassandra(self) -> FrameworkCycle:
+        t_cycle = time.perf_counter()
+        env = _scheduler_env("cassandra", NODE_COUNT="3")
+        cfg, persister, master = self._config(), MemPersister(), self._master(3)
+        runner = None
+        try:
+            t0 = time.perf_counter()
+            runner = self._start(master, env, cfg, persister)
+            api, store = runner.framework_runner.api_server.router, runner.scheduler.state_store
+            self._wait(lambda: api.get("/v1/plans/deploy").status == 200, "cassandra deploy COMPLETE")
+            deploy_s = time.perf_counter() - t0
+            rm = runner.framework_runner.framework_scheduler.offer_processor.revive_manager
+            self._wait(lambda: rm.is_suppressed, "scheduler idle after deploy")
+
+            # replace a seed node (node-1 of 3 is a seed with the default SEED_COUNT of 2)
+            old = store.fetch_task("node-1-server").task_id.value
+            t1 = time.perf_counter()
+            r = api.post("/v1/pod/node-1/replace")
+            if r.status != 200:
+                raise RuntimeError(f"replace failed: {r.status} {r.payload()!r}")
+            self._wait(lambda: self._ready(store, "node-1-server", old) and
+                       api.get("/v1/plans/recovery").status == 200, "cassandra replace recovery")
+            replace_s = time.perf_counter() - t1
+            cmd = store.fetch_task("node-1-server").command.value
+            if "-Dcassandra.replace_address=" not in cmd:
+                raise RuntimeError("replacement did not go through CassandraRecoveryPlanOverrider")
+            tasks = sum(1 for n in store.fetch_task_names()
+                        if (store.fetch_status(n) or P.TaskStatus()).state == P.TASK_RUNNING)
+        finally:
+            if runner is not None:
+                runner.stop()
+            master.shutdown()
+        return FrameworkCycle("cassandra", deploy_s, replace_s, "mttr_replace_node_s", tasks,
+                              time.perf_counter() - t_cycle)
+
+    def _hdfs(self) -> FrameworkCycle:
+        t_cycle = time.perf_counter()
+        env = _scheduler_env("hdfs")
+        cfg, persister, master = self._config(), MemPersister(), self._master(8)
+        runner = None
+        try:
+            t0 = time.perf_counter()
+            runner = self._start(master, env, cfg, persister)
+            api = runner.framework_runner.api_server.router
+            self._wait(lambda: api.get("/v1/plans/deploy").status == 200, "hdfs deploy COMPLETE")
+            deploy_s = time.perf_counter() - t0
+            store = runner.scheduler.state_store
+            # the scheduler records deploy completion on its next status pass; a later config
+            # change is then rolled out by the update plan instead of re-running deploy
+            self._wait(lambda: get_deployment_was_completed(store), "deploy-completed marker")
+            running = [n for n in store.fetch_task_names()
+                       if (store.fetch_status(n) or P.TaskStatus()).state == P.TASK_RUNNING]
+            before = {n: store.fetch_task(n).task_id.value for n in running}
+            runner.stop()
+            runner = None
+
+            # configuration change routed to every task (TASKCFG_ALL_*): the update plan restarts all
+            env2 = dict(env, TASKCFG_ALL_BENCH_ROLLOUT="2")
+            t1 = time.perf_counter()
+            runner = self._start(master, env2, cfg, persister)
+            api, store = runner.framework_runner.api_server.router, runner.scheduler.state_store
+            plan = runner.scheduler.get_plan("deploy")
+            if plan is None or [p.get_name() for p in plan.get_children()] != ["journal", "name", "data"]:
+                raise RuntimeError("update plan was not selected for the configuration change: %r" % (
+                    plan and [p.get_name() for p in plan.get_children()],))
+            self._wait(lambda: api.get("/v1/plans/deploy").status == 200 and
+                       all(self._ready(store, n, old) for n, old in before.items()), "hdfs rolling update")
+            update_s = time.perf_counter() - t1
+            tasks = len(before)
+        finally:
+            if runner is not None:
+                runner.stop()
+            master.shutdown()
+        return FrameworkCycle("hdfs", deploy_s, update_s, "rolling_update_s", tasks, time.perf_counter() - t_cycle)
+
+
+def main(argv: Optional[List[str]] = None) -> int:
+    import argparse
+    import json
+
+    ap = argparse.ArgumentParser(description="cassandra / hdfs framework benchmarks (BASELINE configs 3 and 4)")
+    ap.add_argument("--framework", choices=["cassandra", "hdfs", "all"], default="all")
+    ap.add_argument("--profile", choices=sorted(PROFILES), default="mi355x")
+    ap.add_argument("--cycles", type=int, default=3)
+    ap.add_argument("--allocation-interval", type=float, default=1.0)
+    args = ap.parse_args(argv)
+    for fw in (["cassandra", "hdfs"] if args.framework == "all" else [args.framework]):
+        bench = FrameworkBench(fw, args.profile, args.allocation_interval)
+        cycles = [bench.run_cycle() for _ in range(args.cycles)]
+        second = cycles[0].second_name
+        out = {"framework": fw, "profile": args.profile, "cycles": args.cycles, "tasks": cycles[0].tasks,
+               "deploy_s": {"mean": round(sum(c.deploy_s for c in cycles) / len(cycles), 6),
+                            "max": round(max(c.deploy_s for c in cycles), 6)},
+               second: {"mean": round(sum(c.second_s for c in cycles) / len(cycles), 6),
+                        "max": round(max(c.second_s for c in cycles), 6)},
+               "data": "synthetic task payloads (LocalMaster), readiness delays not honoured"}
+        print(json.dumps(out), flush=True)
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())

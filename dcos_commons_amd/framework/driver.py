@@ -2,8 +2,8 @@
 
 Reference: sdk/.../framework/Driver.java (global ``SchedulerDriver`` singleton) and the
 ``org.apache.mesos.SchedulerDriver`` interface. Implementations:
-* ``dcos_commons_amd.mesos.v1_client.V1SchedulerDriver`` -- Mesos v1 HTTP scheduler API;
-* ``dcos_commons_amd.mesos.fake_master.FakeMasterDriver`` -- in-process fake master;
+* ``dcos_commons_amd.mesos.http_driver.V1HttpSchedulerDriver`` -- Mesos v1 HTTP scheduler API;
+* ``dcos_commons_amd.mesos.local_master.LocalSchedulerDriver`` -- in-process Mesos master;
 * ``dcos_commons_amd.testing.RecordingDriver`` -- records calls for simulation tests.
 """
 from __future__ import annotations

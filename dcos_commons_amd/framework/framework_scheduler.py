@@ -34,12 +34,14 @@ class FrameworkScheduler:
         self.client = client
         self.offer_processor = offer_processor or OfferProcessor(
             client, persister, scheduler_config,
-            token_bucket=TokenBucket(acquire_interval_s=scheduler_config.revive_interval_s())
+            token_bucket=TokenBucket(acquire_interval_s=scheduler_config.revive_interval_s(),
+                                     burst_interval_s=scheduler_config.revive_burst_interval_s())
             if scheduler_config is not None else None,
             hold_s=scheduler_config.offer_hold_s() if scheduler_config is not None else 0.0,
             event_driven=scheduler_config.is_event_driven() if scheduler_config is not None else False,
             gc_all_offers=scheduler_config.is_reservation_gc_on_all_offers() if scheduler_config is not None else False,
-            fast_unsuppress=scheduler_config.is_fast_unsuppress() if scheduler_config is not None else False)
+            fast_unsuppress=scheduler_config.is_fast_unsuppress() if scheduler_config is not None else False,
+            merge_agent_offers=scheduler_config.is_merge_agent_offers() if scheduler_config is not None else False)
         if implicit_reconciler is None:
             implicit_reconciler = ImplicitReconciler(
                 scheduler_config.implicit_reconcile_delay_s() if scheduler_config is not None else 0.0,

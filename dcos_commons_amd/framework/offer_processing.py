@@ -18,7 +18,7 @@ import collections
 import logging
 import threading
 import time
-from typing import Callable, Dict, List, Optional
+from typing import Callable, Dict, List, Optional, Tuple
 
 from dcos_commons_amd import metrics
 from dcos_commons_amd.mesos import protos as P
@@ -94,12 +94,25 @@ class OfferQueue:
 
 
 class TokenBucket:
-    """Revive rate limiter: capacity 256, +1 token every 256 s, >= 5 s between acquires."""
+    """Revive rate limiter: capacity 256, +1 token every 256 s, >= 5 s between acquires
+    (TokenBucket.java:17-24,81).
+
+    ``burst_interval_s`` (default: same as ``acquire_interval_s``, i.e. the reference's flat
+    spacing) applies instead of ``acquire_interval_s`` while more than ``burst_floor`` tokens
+    (default half the capacity) remain: a healthy bucket lets a burst of new work revive promptly,
+    a bucket drained by a crash loop falls back to the slow spacing. The capacity and refill rate
+    bound the sustained rate either way.
+    """
 
     def __init__(self, initial: int = 256, capacity: int = 256, increment_interval_s: float = 256.0,
-                 acquire_interval_s: float = 5.0, clock: Callable[[], float] = time.monotonic):
+                 acquire_interval_s: float = 5.0, clock: Callable[[], float] = time.monotonic,
+                 burst_interval_s: Optional[float] = None, burst_floor: Optional[int] = None):
         if initial < 0 or capacity < 1 or increment_interval_s <= 0 or acquire_interval_s < 0:
             raise ValueError("TokenBucket construction failed with invalid configuration")
+        if burst_interval_s is not None and not 0 <= burst_interval_s <= acquire_interval_s:
+            raise ValueError("TokenBucket burst interval must be within [0, acquire interval]")
+        self.burst_interval_s = acquire_interval_s if burst_interval_s is None else burst_interval_s
+        self.burst_floor = capacity // 2 if burst_floor is None else burst_floor
         self.initial = initial
         self.count = initial
         self.capacity = capacity
@@ -117,12 +130,15 @@ class TokenBucket:
             self.count = min(self.capacity, self.count + n)
             self._last_increment += n * self.increment_interval_s
 
+    def _spacing(self) -> float:
+        return self.burst_interval_s if self.count > self.burst_floor else self.acquire_interval_s
+
     def try_acquire(self, ignore_spacing: bool = False) -> bool:
         with self._lock:
             self._refill()
             now = self.clock()
             if self.count > 0 and (ignore_spacing or self._last_acquire is None or
-                                   now - self._last_acquire >= self.acquire_interval_s):
+                                   now - self._last_acquire >= self._spacing()):
                 self.count -= 1
                 self._last_acquire = now
                 return True
@@ -135,7 +151,7 @@ class TokenBucket:
             now = self.clock()
             wait = 0.0
             if self._last_acquire is not None:
-                wait = max(0.0, self.acquire_interval_s - (now - self._last_acquire))
+                wait = max(0.0, self._spacing() - (now - self._last_acquire))
             if self.count <= 0:
                 wait = max(wait, self.increment_interval_s - (now - self._last_increment))
             return wait
@@ -211,7 +227,10 @@ class OfferAccepter:
             out.setdefault(r.agent_id.value, []).append(r)
         return dict(sorted(out.items()))
 
-    def accept(self, recs) -> None:
+    def accept(self, recs, members: Optional[Dict[str, List[P.Offer]]] = None) -> None:
+        """``members``: merged offer id -> the real offers it stands for (``merge_agent_offers``);
+        an ACCEPT on a merged offer names every member (Mesos accepts several offers of one agent
+        in one call)."""
         if not recs:
             return
         d = driver.get_instance()
@@ -222,9 +241,11 @@ class OfferAccepter:
                 if op is None:
                     continue
                 ops.append(op)
-                if r.offer_id.value not in seen:
-                    seen.add(r.offer_id.value)
-                    offer_ids.append(r.offer_id)
+                group = members.get(r.offer_id.value) if members else None
+                for oid in ([o.id for o in group] if group else [r.offer_id]):
+                    if oid.value not in seen:
+                        seen.add(oid.value)
+                        offer_ids.append(oid)
             if not ops:
                 continue
             LOGGER.info("Sending %d operation(s) for agent %s: %s", len(ops), agent,
@@ -283,6 +304,52 @@ def recycled_offers(offers, offer_resources_list):
     return out
 
 
+def merge_agent_offers(offers) -> Tuple[List[P.Offer], Dict[str, List[P.Offer]]]:
+    """One evaluation unit per agent: offers of the same agent are combined into a copy of the
+    first (resources merged the way the master would, executor ids unioned). Returns the offers to
+    evaluate and ``{merged id: [member offers]}`` for every agent that had more than one.
+
+    Why: an agent's resources can be split across outstanding offers (a held offer plus the
+    resources a finished task released, offered separately). A step that needs both (e.g. a pod's
+    own reservation plus new unreserved resources for its next resource set) passes on neither
+    offer alone, and would wait until the held one is declined and re-offered whole. The
+    reference evaluates offers one at a time (OfferEvaluator.java:113-248) but does not hold them.
+    """
+    from dcos_commons_amd.mesos.resource_math import ResourceBag
+
+    by_agent: Dict[str, List[P.Offer]] = {}
+    for o in offers:
+        by_agent.setdefault(o.agent_id.value, []).append(o)
+    out: List[P.Offer] = []
+    members: Dict[str, List[P.Offer]] = {}
+    for group in by_agent.values():
+        if len(group) == 1:
+            out.append(group[0])
+            continue
+        m = P.Offer()
+        m.CopyFrom(group[0])
+        del m.resources[:]
+        del m.executor_ids[:]
+        bag, alloc, execs = ResourceBag(), None, []
+        for o in group:
+            for r in o.resources:
+                if alloc is None and r.HasField("allocation_info"):
+                    alloc = r.allocation_info
+                bag.add(r)
+            for e in o.executor_ids:
+                if e.value not in execs:
+                    execs.append(e.value)
+        for r in bag.to_resources():
+            if alloc is not None:
+                r.allocation_info.CopyFrom(alloc)
+            m.resources.add().CopyFrom(r)
+        for e in execs:
+            m.executor_ids.add(value=e)
+        members[m.id.value] = list(group)
+        out.append(m)
+    return out, members
+
+
 def _targeted_resource_ids(recs) -> set:
     from dcos_commons_amd.offer.resources import get_resource_id
 
@@ -330,7 +397,7 @@ class OfferProcessor:
     def __init__(self, client, persister, scheduler_config=None, token_bucket: Optional[TokenBucket] = None,
                  queue_capacity: int = DEFAULT_QUEUE_CAPACITY, offer_wait_s: Optional[float] = None,
                  hold_s: float = 0.0, event_driven: bool = False, gc_all_offers: bool = False,
-                 fast_unsuppress: bool = False):
+                 fast_unsuppress: bool = False, merge_agent_offers: bool = False):
         self.client = client
         self.persister = persister
         self.offer_wait_s = offer_wait_s if offer_wait_s is not None else (
@@ -347,7 +414,8 @@ class OfferProcessor:
         # onto the same agent, or a scheduler that goes idle, leaks them until the next work.
         # gc_all_offers collects them from every offer, idle or not.
         self.gc_all_offers = gc_all_offers
-        self._held: Dict[str, tuple] = {}  # offer id -> (offer, hold deadline)
+        self.merge_agent_offers = merge_agent_offers
+        self._held: Dict[str, tuple] = {}  # (real) offer id -> (offer, hold deadline)
         self._initialized = False
         self._deregistered = False
         self._in_progress = set()
@@ -482,6 +550,13 @@ class OfferProcessor:
         return filter_out_accepted(offers, recs)
 
     def _evaluate(self, offers, now: float) -> None:
+        members: Dict[str, List[P.Offer]] = {}
+        if self.merge_agent_offers:
+            offers, members = merge_agent_offers(offers)
+
+        def real(os_):
+            return [m for o in os_ for m in members.get(o.id.value, (o,))]
+
         pre_cleanup = []
         cleanup_result = UnexpectedResult.PROCESSED
         eval_offers = offers
@@ -504,9 +579,10 @@ class OfferProcessor:
             cleanup_result = un.result
             cleanup_recs = to_cleanup_recommendations(un.offer_resources)
             unused = filter_out_accepted(unused, cleanup_recs)
-        used = {o.id.value for o in offers} - {o.id.value for o in unused}
+        used = {o.id.value for o in real(offers)} - {o.id.value for o in real(unused)}
         for oid in used:
             self._held.pop(oid, None)
+        unused = real(unused)
         if unused:
             if resp.result == OfferResult.PROCESSED and cleanup_result == UnexpectedResult.PROCESSED:
                 if self.hold_s > 0:
@@ -528,7 +604,7 @@ class OfferProcessor:
                 decline_short(unused)
         all_recs = pre_cleanup + list(resp.recommendations) + cleanup_recs
         metrics.increment_recommendations(all_recs)
-        self.accepter.accept(all_recs)
+        self.accepter.accept(all_recs, members)
 
     def release_held(self) -> None:
         """Decline every held offer (e.g. when the scheduler goes idle or stops)."""

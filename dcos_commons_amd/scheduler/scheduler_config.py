@@ -238,10 +238,22 @@ class SchedulerConfig:
         costs the master little and takes up to 4 s off every recovery that needs a revive."""
         return self.env.get_optional_double("SDK_REVIVE_INTERVAL_S", 1.0)
 
+    def revive_burst_interval_s(self) -> float:
+        """REVIVE spacing while the revive token bucket is more than half full (a burst of new
+        candidate steps, e.g. a pod relaunching in place after its ONCE task finished, gets its
+        offers within one allocation instead of waiting out ``SDK_REVIVE_INTERVAL_S``). Clamped
+        to the revive interval; the reference has no burst regime."""
+        return min(self.env.get_optional_double("SDK_REVIVE_BURST_INTERVAL_S", 0.05), self.revive_interval_s())
+
     def is_reservation_gc_on_all_offers(self) -> bool:
         """Release stale reservations from every offer, idle or not (reference: unused offers
         while WORKING only)."""
         return self.env.get_optional_boolean("SDK_RESERVATION_GC_ALL_OFFERS", True)
+
+    def is_merge_agent_offers(self) -> bool:
+        """Evaluate all outstanding offers of one agent as a single offer and ACCEPT them together
+        (reference: every offer on its own)."""
+        return self.env.get_optional_boolean("SDK_MERGE_AGENT_OFFERS", True)
 
     def is_fast_unsuppress(self) -> bool:
         """First REVIVE after a SUPPRESS skips the burst spacing (reference: never)."""

@@ -457,8 +457,8 @@ class ZkClient:
             if time.monotonic() - self._last_send > self.negotiated_timeout_ms / 3000.0:
                 try:
                     self._send_frame(Writer().int(XID_PING).int(OP_PING).bytes())
-                except OSError:
-                    pass
+                except (OSError, ConnectionLossError):
+                    pass  # the connection dropped between the check and the send: the reader reconnects
 
     def _send_frame(self, payload: bytes) -> None:
         with self._send_lock:
