@@ -208,7 +208,9 @@ def main(argv=None) -> int:
     argv = sys.argv[1:] if argv is None else argv
     if len(argv) != 1:
         raise SystemExit(f"Expected one file argument, got: {argv}")
-    logging.basicConfig(level=os.environ.get("FRAMEWORK_LOG_LEVEL", "INFO"))
+    from dcos_commons_amd.utils import logging_utils
+
+    logging_utils.configure()
     SchedulerRunner.from_scheduler_builder(create_scheduler_builder(argv[0])).run()
     return 0
 

@@ -271,7 +271,9 @@ def run(args: List[str], env: Optional[Dict[str, str]] = None, scheduler_config=
 
 
 def main(argv=None) -> int:
-    logging.basicConfig(level=os.environ.get("FRAMEWORK_LOG_LEVEL", "INFO"))
+    from dcos_commons_amd.utils import logging_utils
+
+    logging_utils.configure()
     run(sys.argv[1:] if argv is None else argv)
     return 0
 

@@ -23,6 +23,7 @@ from dcos_commons_amd.offer.resources import get_resource_id
 from dcos_commons_amd.offer.taskdata.labels import TaskException, TaskLabelReader
 from dcos_commons_amd.scheduler.plan.pod_instance_requirement import PodInstanceRequirement, RecoveryType
 from dcos_commons_amd.specification.specs import GoalState, NamedVIPSpec, PortSpec, ResourceSpec
+from dcos_commons_amd.utils.logging_utils import get_logger
 
 from .pod_info_builder import PodInfoBuilder
 from .resource_mappers import ExecutorResourceMapper, TaskResourceMapper
@@ -84,7 +85,7 @@ class OfferEvaluator:
         self.offer_outcome_tracker_v2 = offer_outcome_tracker_v2
         self.tls_stage_factory = tls_stage_factory
         self._framework_id: Optional[str] = None
-        self.logger = logging.getLogger(__name__ + (f"({resource_namespace})" if resource_namespace else ""))
+        self.logger = get_logger(__name__, resource_namespace)
 
     def _fid(self) -> P.FrameworkID:
         fid = self.framework_store.fetch_framework_id()

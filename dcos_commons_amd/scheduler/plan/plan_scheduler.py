@@ -12,6 +12,7 @@ from typing import List, Optional
 
 from dcos_commons_amd.framework import task_killer
 from dcos_commons_amd.offer.task_utils import is_terminal
+from dcos_commons_amd.utils.logging_utils import get_logger
 
 LOGGER = logging.getLogger(__name__)
 
@@ -20,7 +21,7 @@ class PlanScheduler:
     def __init__(self, offer_evaluator, state_store, namespace: Optional[str] = None):
         self.offer_evaluator = offer_evaluator
         self.state_store = state_store
-        self.logger = logging.getLogger(__name__ + (f"({namespace})" if namespace else ""))
+        self.logger = get_logger(__name__, namespace)
 
     def resource_offers(self, offers, steps) -> list:
         all_recs = []

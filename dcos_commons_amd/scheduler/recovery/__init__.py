@@ -25,6 +25,7 @@ from dcos_commons_amd.scheduler.plan.elements import DefaultPhase, DefaultPlan, 
 from dcos_commons_amd.scheduler.plan.managers import PlanManager
 from dcos_commons_amd.scheduler.plan.pod_instance_requirement import PodInstanceRequirement, RecoveryType
 from dcos_commons_amd.scheduler.plan.strategy import ParallelStrategy
+from dcos_commons_amd.utils.logging_utils import get_logger
 
 DEFAULT_RECOVERY_PHASE_NAME = "default"
 
@@ -144,7 +145,7 @@ class DefaultRecoveryPlanManager(PlanManager):
         self.overriders = list(overriders or [])
         self._plan = DefaultPlan(constants.RECOVERY_PLAN_NAME, [], ParallelStrategy())
         self._lock = threading.RLock()
-        self.logger = logging.getLogger(__name__ + (f"({namespace})" if namespace else ""))
+        self.logger = get_logger(__name__, namespace)
 
     def get_plan(self):
         with self._lock:
