@@ -156,3 +156,4 @@ def test_accepter_names_every_member_offer():
     finally:
         driver.set_driver(None)
     assert calls == [["o1", "o2"]]
+
