@@ -90,6 +90,14 @@ class DeployBench:
             time.sleep(0.001)
 
     @staticmethod
+    def _plan_done(scheduler, name: str) -> bool:
+        """What ``GET /v1/plans/<name>`` reports as 200 (COMPLETE, no errors), read straight from
+        the plan instead of rendering the plan JSON through the API router on every 1 ms poll (the
+        poller would otherwise compete with the scheduler it is timing)."""
+        plan = scheduler.get_plan(name)
+        return plan is not None and not plan.has_errors() and plan.is_complete()
+
+    @staticmethod
     def _pod_ready(state_store, task_name: str, old_task_id: Optional[str]) -> bool:
         info = state_store.fetch_task(task_name)
         st = state_store.fetch_status(task_name)
@@ -100,6 +108,12 @@ class DeployBench:
         if st.task_id.value != info.task_id.value:
             return False
         return TaskLabelReader(info).is_readiness_check_succeeded(st)
+
+    @staticmethod
+    def _expect_api(router, plan: str) -> None:
+        r = router.get(f"/v1/plans/{plan}")
+        if r.status != 200:
+            raise RuntimeError(f"/v1/plans/{plan} answered {r.status} after the plan completed")
 
     def _make_master(self) -> LocalMaster:
         behavior = TaskBehavior(TaskTiming(), check_runner=self.check_runner)
@@ -131,8 +145,10 @@ class DeployBench:
             runner.run(block=False)
             router = runner.framework_runner.api_server.router
             state_store = runner.scheduler.state_store
-            self._wait(lambda: router.get("/v1/plans/deploy").status == 200, "deploy plan COMPLETE")
+            sched = runner.scheduler
+            self._wait(lambda: self._plan_done(sched, "deploy"), "deploy plan COMPLETE")
             deploy_s = time.perf_counter() - t0
+            self._expect_api(router, "deploy")
 
             # failures are injected in steady state: deploy finished and the offer loop has gone
             # idle (suppressed), as for a pod that fails long after its service deployed
@@ -144,8 +160,9 @@ class DeployBench:
             t1 = time.perf_counter()
             master.fail_task(old)
             self._wait(lambda: self._pod_ready(state_store, "hello-0-server", old) and
-                       router.get("/v1/plans/recovery").status == 200, "restart recovery")
+                       self._plan_done(sched, "recovery"), "restart recovery")
             mttr_restart = time.perf_counter() - t1
+            self._expect_api(router, "recovery")
 
             self._wait(lambda: rm.is_suppressed, "scheduler idle after restart")
 
@@ -156,8 +173,9 @@ class DeployBench:
             if r.status != 200:
                 raise RuntimeError(f"replace failed: {r.status} {r.payload()!r}")
             self._wait(lambda: self._pod_ready(state_store, "hello-0-server", old) and
-                       router.get("/v1/plans/recovery").status == 200, "replace recovery")
+                       self._plan_done(sched, "recovery"), "replace recovery")
             mttr_replace = time.perf_counter() - t2
+            self._expect_api(router, "recovery")
         finally:
             runner.stop()
             master.shutdown()

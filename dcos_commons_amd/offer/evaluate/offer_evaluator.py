@@ -69,6 +69,22 @@ def _outcome_reasons(out: List[str], outcome) -> None:
         _outcome_reasons(out, c)
 
 
+class _LazyText:
+    """Renders on first ``str()`` (log formatting) or ``render()`` (debug trackers), once."""
+
+    __slots__ = ("_fn", "_text")
+
+    def __init__(self, fn):
+        self._fn, self._text = fn, None
+
+    def render(self) -> str:
+        if self._text is None:
+            self._text = self._fn()
+        return self._text
+
+    __str__ = render
+
+
 class OfferEvaluator:
     def __init__(self, framework_store, state_store, service_name: str, target_config_id, template_url_factory,
                  scheduler_config, resource_namespace: Optional[str] = None,
@@ -122,19 +138,17 @@ class OfferEvaluator:
                 outcomes.append(o)
                 if not o.passing:
                     failed += 1
-            details_lines: List[str] = []
-            for o in outcomes:
-                details_lines.extend(_outcome_lines(o))
-            details = "\n".join(details_lines)
+            details = _LazyText(lambda outcomes=outcomes: "\n".join(
+                line for o in outcomes for line in _outcome_lines(o)))
             if failed:
                 self.logger.info("Offer %d, %s: failed %d of %d evaluation stages for %s:\n%s", i + 1,
                                  offer.id.value, failed, len(stages), requirement.name, details)
-                self._track(requirement, False, offer, details, outcomes)
+                self._track(requirement, False, offer, details.render, outcomes)
                 continue
             recs = [r for o in outcomes for r in o.get_offer_recommendations()]
             self.logger.info("Offer %d: passed all %d evaluation stages, returning %d recommendations for %s",
                              i + 1, len(stages), len(recs), requirement.name)
-            self._track(requirement, True, offer, details, outcomes)
+            self._track(requirement, True, offer, details.render, outcomes)
             return recs
         return []
 
@@ -142,9 +156,12 @@ class OfferEvaluator:
         if self.offer_outcome_tracker is not None:
             self.offer_outcome_tracker.track(OfferOutcome(requirement.name, passed, offer, details))
         if self.offer_outcome_tracker_v2 is not None:
-            reasons: List[str] = []
-            for o in outcomes:
-                _outcome_reasons(reasons, o)
+            def reasons(outcomes=outcomes) -> List[str]:
+                out: List[str] = []
+                for o in outcomes:
+                    _outcome_reasons(out, o)
+                return out
+
             s = self.offer_outcome_tracker_v2.summary
             s.add_offer(OfferOutcome(requirement.name, passed, offer, reasons))
             if not passed:

@@ -17,14 +17,23 @@ DEFAULT_CAPACITY = 100
 
 
 class OfferOutcome:
-    __slots__ = ("timestamp", "pod_instance_name", "passed", "offer", "details")
+    """``details`` may be given as a zero-argument callable: it is rendered (once) when a debug
+    endpoint reads it, not on the offer-evaluation path."""
+
+    __slots__ = ("timestamp", "pod_instance_name", "passed", "offer", "_details")
 
     def __init__(self, pod_instance_name: str, passed: bool, offer: P.Offer, details):
         self.timestamp = int(time.time() * 1000)
         self.pod_instance_name = pod_instance_name
         self.passed = passed
         self.offer = offer
-        self.details = details
+        self._details = details
+
+    @property
+    def details(self):
+        if callable(self._details):
+            self._details = self._details()
+        return self._details
 
 
 class OfferOutcomeTracker:

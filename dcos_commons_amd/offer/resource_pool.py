@@ -15,7 +15,7 @@ from dcos_commons_amd.mesos import protos as P
 from dcos_commons_amd.specification.specs import ANY_ROLE, VolumeSpec
 
 from . import values as V
-from .resources import MesosResource, ResourceBuilder, get_disk_source
+from .resources import MesosResource, ResourceBuilder, get_disk_source, unreserved_resource
 
 LOGGER = logging.getLogger(__name__)
 
@@ -104,7 +104,7 @@ class MesosResourcePool:
         if not V.sufficient(desired, available):
             return None
         pool[name] = V.subtract(available, desired)
-        r = ResourceBuilder.from_unreserved_value(name, desired).build()
+        r = unreserved_resource(name, desired)
         if capabilities.get_instance().supports_pre_reserved_resources and pre_reserved_role != ANY_ROLE:
             r.reservations.add(role=pre_reserved_role, type=P.Resource.ReservationInfo.STATIC)
         return MesosResource(r)

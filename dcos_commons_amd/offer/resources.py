@@ -6,7 +6,6 @@ carry the labels ``resource_id``, ``framework_id`` and ``namespace`` on their (l
 """
 from __future__ import annotations
 
-import uuid
 from typing import Iterable, List, Optional
 
 from dcos_commons_amd.dcos import capabilities
@@ -19,6 +18,7 @@ from dcos_commons_amd.specification.specs import (
     VolumeSpec,
     VolumeType,
 )
+from dcos_commons_amd.utils.ids import uuid4_str
 
 from . import values as V
 
@@ -189,11 +189,12 @@ class MesosResource:
 # ResourceBuilder
 
 
-def _set_value(r: P.Resource, value: P.Value) -> None:
+def _set_value(r: P.Resource, value: P.Value, fresh: bool = False) -> None:
     r.type = value.type
-    r.ClearField("scalar")
-    r.ClearField("ranges")
-    r.ClearField("set")
+    if not fresh:
+        r.ClearField("scalar")
+        r.ClearField("ranges")
+        r.ClearField("set")
     if value.type == P.Value.SCALAR:
         r.scalar.CopyFrom(value.scalar)
     elif value.type == P.Value.RANGES:
@@ -202,6 +203,14 @@ def _set_value(r: P.Resource, value: P.Value) -> None:
         r.set.CopyFrom(value.set)
     else:
         raise ValueError(f"Unsupported spec value type: {value.type}")
+
+
+def unreserved_resource(name: str, value: P.Value) -> P.Resource:
+    """``ResourceBuilder.from_unreserved_value(name, value).build()`` without the builder: an
+    unreserved ``*`` resource (the pool's view of what a consumption took from an offer)."""
+    r = P.Resource(name=name, role=ANY_ROLE)
+    _set_value(r, value, True)
+    return r
 
 
 class ResourceBuilder:
@@ -302,19 +311,26 @@ class ResourceBuilder:
         self.mesos_resource = mr
         return self
 
+    def _reservation_labels(self, labels: P.Labels) -> None:
+        """resource_id / framework_id / namespace labels, in the key order ``map_to_labels`` writes."""
+        kv = {L.RESOURCE_ID_RESERVATION_LABEL: self.resource_id or uuid4_str()}
+        if self.framework_id is not None:
+            kv[L.FRAMEWORK_ID_RESERVATION_LABEL] = self.framework_id
+        if self.resource_namespace is not None:
+            kv[L.NAMESPACE_RESERVATION_LABEL] = self.resource_namespace
+        for k in sorted(kv):
+            labels.labels.add(key=k, value=kv[k])
+
     def _reservation(self) -> P.Resource.ReservationInfo:
         r = P.Resource.ReservationInfo(role=self.role, type=P.Resource.ReservationInfo.DYNAMIC,
                                        principal=self.principal or "")
-        L.set_reservation_label(r, L.RESOURCE_ID_RESERVATION_LABEL, self.resource_id or str(uuid.uuid4()))
-        if self.framework_id is not None:
-            L.set_reservation_label(r, L.FRAMEWORK_ID_RESERVATION_LABEL, self.framework_id)
-        if self.resource_namespace is not None:
-            L.set_reservation_label(r, L.NAMESPACE_RESERVATION_LABEL, self.resource_namespace)
+        self._reservation_labels(r.labels)
         return r
 
     def build(self) -> P.Resource:
         r = P.Resource()
-        if self.mesos_resource is not None:
+        fresh = self.mesos_resource is None
+        if not fresh:
             r.CopyFrom(self.mesos_resource.resource)
             r.ClearField("allocation_info")
         r.name = self.name
@@ -326,15 +342,12 @@ class ResourceBuilder:
             if pre_reserved_supported:
                 if self.pre_reserved_role != ANY_ROLE and self.mesos_resource is None:
                     r.reservations.add(role=self.pre_reserved_role, type=P.Resource.ReservationInfo.STATIC)
-                r.reservations.add().CopyFrom(self._reservation())
+                res = r.reservations.add(role=self.role, type=P.Resource.ReservationInfo.DYNAMIC,
+                                         principal=self.principal or "")
+                self._reservation_labels(res.labels)
             else:
-                legacy = P.Resource.ReservationInfo(principal=self.principal or "")
-                L.set_reservation_label(legacy, L.RESOURCE_ID_RESERVATION_LABEL, self.resource_id or str(uuid.uuid4()))
-                if self.framework_id is not None:
-                    L.set_reservation_label(legacy, L.FRAMEWORK_ID_RESERVATION_LABEL, self.framework_id)
-                if self.resource_namespace is not None:
-                    L.set_reservation_label(legacy, L.NAMESPACE_RESERVATION_LABEL, self.resource_namespace)
-                r.reservation.CopyFrom(legacy)
+                r.reservation.principal = self.principal or ""
+                self._reservation_labels(r.reservation.labels)
         if self.role is not None and not pre_reserved_supported:
             r.role = self.role
         elif pre_reserved_supported and len(r.reservations) > 0:
@@ -345,8 +358,8 @@ class ResourceBuilder:
             r.disk.volume.container_path = self.disk_container_path
             r.disk.volume.mode = P.Volume.RW
             r.disk.persistence.principal = self.principal or ""
-            r.disk.persistence.id = self.disk_persistence_id or str(uuid.uuid4())
+            r.disk.persistence.id = self.disk_persistence_id or uuid4_str()
             if self.disk_source is not None:
                 r.disk.source.CopyFrom(self.disk_source)
-        _set_value(r, self.value)
+        _set_value(r, self.value, fresh)
         return r
