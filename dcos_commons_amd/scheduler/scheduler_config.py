@@ -47,6 +47,8 @@ class SchedulerConfig:
             "PACKAGE_BUILD_TIME_EPOCH_MS": "0",
             "LIBPROCESS_IP": "127.0.0.1",
             "DISABLE_DEADLOCK_EXIT": "true",
+            # tests never share an on-disk state tree (or its lock) through the working directory
+            "SDK_PERSISTER": "mem",
         }
         env.update({k: str(v) for k, v in overrides.items()})
         return SchedulerConfig(EnvStore.from_map(env))
