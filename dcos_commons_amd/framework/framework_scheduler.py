@@ -11,7 +11,7 @@ from __future__ import annotations
 import logging
 import threading
 
-from dcos_commons_amd import metrics
+from dcos_commons_amd import metrics, trace
 from dcos_commons_amd.mesos import protos as P
 from dcos_commons_amd.offer import resources as ResourceUtils
 from dcos_commons_amd.offer.evaluate.placement import IsLocalRegionRule
@@ -134,7 +134,8 @@ class FrameworkScheduler:
             LOGGER.info("Received status update for taskId=%s state=%s message='%s'", status.task_id.value,
                         P.TaskState.Name(status.state), status.message)
             metrics.record_status(status)
-            resp = self.client.task_status(status)
+            with trace.span("status", "status", task=status.task_id.value, state=P.TaskState.Name(status.state)):
+                resp = self.client.task_status(status)
             eligible = task_killer.update(status)
             if resp.result == TaskStatusResult.UNKNOWN_TASK:
                 if eligible:

@@ -20,7 +20,7 @@ import threading
 import time
 from typing import Callable, Dict, List, Optional, Tuple
 
-from dcos_commons_amd import metrics
+from dcos_commons_amd import metrics, trace
 from dcos_commons_amd.mesos import protos as P
 from dcos_commons_amd.offer import constants
 from dcos_commons_amd.offer.recommendations import DestroyOfferRecommendation, UnreserveOfferRecommendation
@@ -233,6 +233,10 @@ class OfferAccepter:
         in one call)."""
         if not recs:
             return
+        with trace.span("accept", "offers", recs=len(recs)):
+            self._accept(recs, members)
+
+    def _accept(self, recs, members) -> None:
         d = driver.get_instance()
         for agent, agent_recs in self.group_by_agent(recs).items():
             ops, offer_ids, seen = [], [], set()
@@ -506,9 +510,11 @@ class OfferProcessor:
                 return
             if self._deregistered:
                 return
-            with metrics.process_offers_timer():
+            with metrics.process_offers_timer(), trace.span("offer_cycle", "offers", new=len(new_offers),
+                                                               held=len(held)) as sp:
                 if self._check_status():
                     self._evaluate(offers, now)
+                    sp.set(working=True)
                 elif offers:
                     self._held.clear()
                     if self.gc_all_offers:

@@ -15,7 +15,7 @@ import re
 import uuid
 from typing import Dict, List, Optional
 
-from dcos_commons_amd import metrics
+from dcos_commons_amd import metrics, trace
 from dcos_commons_amd.debug import PlansTracker, TaskReservationsTracker, TaskStatusesTracker, thread_dump
 from dcos_commons_amd.framework import task_killer
 from dcos_commons_amd.http import endpoint_utils
@@ -779,7 +779,22 @@ class DebugResource:
             Route("GET", "/v1/debug/plans", lambda r: json_ok(self.plans_tracker.get_json(*f(r)))),
             Route("GET", "/v1/debug/taskStatuses", lambda r: json_ok(self.statuses_tracker.get_json(*f(r)))),
             Route("GET", "/v1/debug/reservations", lambda r: json_ok(self.reservations_tracker.get_json(*f(r)))),
+            Route("GET", "/v1/debug/trace", self.trace),
         ]
+
+    @staticmethod
+    def trace(req: Request) -> Response:
+        """Chrome trace of the offer cycles, step evaluations, status updates and persister ops
+        (``?enable=true`` / ``?enable=false`` toggles recording, ``?summary=true`` aggregates per
+        span name, ``?clear=true`` empties the ring after reading)."""
+        en = req.q("enable")
+        if en is not None:
+            trace.enable() if en.lower() in ("1", "true", "yes") else trace.disable()
+        body = {"spans": trace.TRACER.summary(), "enabled": trace.enabled()} if req.q_bool("summary") \
+            else trace.TRACER.to_json()
+        if req.q_bool("clear"):
+            trace.TRACER.clear()
+        return json_ok(body)
 
     def offers(self, req: Request) -> Response:
         tracker = self.scheduler.offer_outcome_tracker

@@ -15,6 +15,7 @@ from __future__ import annotations
 import logging
 from typing import Dict, List, Optional, Sequence
 
+from dcos_commons_amd import trace
 from dcos_commons_amd.mesos import protos as P
 from dcos_commons_amd.offer import task_utils
 from dcos_commons_amd.offer.history import OfferOutcome, OfferOutcomeTracker, OfferOutcomeTrackerV2
@@ -111,6 +112,15 @@ class OfferEvaluator:
 
     def evaluate(self, requirement: PodInstanceRequirement, offers: Sequence[P.Offer],
                  all_tasks: Optional[Dict[str, P.TaskInfo]] = None) -> list:
+        if not trace.enabled():
+            return self._evaluate(requirement, offers, all_tasks)
+        with trace.span("evaluate", "offers", step=requirement.name, offers=len(offers)) as sp:
+            recs = self._evaluate(requirement, offers, all_tasks)
+            sp.set(recs=len(recs))
+            return recs
+
+    def _evaluate(self, requirement: PodInstanceRequirement, offers: Sequence[P.Offer],
+                  all_tasks: Optional[Dict[str, P.TaskInfo]]) -> list:
         fid_proto = self._fid()
         if self._framework_id is None:
             self._framework_id = fid_proto.value

@@ -107,6 +107,10 @@ def persister_for_service(service_spec, scheduler_config) -> Persister:
         init_service_name(base, service_spec.name)
     else:
         raise ValueError(f"Unknown SDK_PERSISTER '{kind}' (expected file, mem or zk)")
+    from dcos_commons_amd import trace
+
+    if trace.enabled():
+        base = trace.TracingPersister(base)
     if scheduler_config.is_state_cache_enabled() and kind != "mem":
         return PersisterCache(base)
     return base
