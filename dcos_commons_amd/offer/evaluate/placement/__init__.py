@@ -199,6 +199,11 @@ def placement_rule_from_dict(d: Optional[dict]) -> Optional[PlacementRule]:
     return cls.from_dict(d)
 
 
+def _opt(v) -> str:
+    """Java ``Optional.toString`` rendering, so rule descriptions read like the reference's."""
+    return "Optional.empty" if v is None else f"Optional[{v}]"
+
+
 def _m(d, key="task-filter"):
     return matcher_from_dict(d.get(key)) if d.get(key) is not None else None
 
@@ -641,6 +646,9 @@ class MaxPerAttributeRule(_MaxPerRule):
     def from_dict(cls, d):
         return cls(d["max"], matcher_from_dict(d["matcher"]), _m(d))
 
+    def __repr__(self):
+        return f"MaxPerAttributeRule{{max={self.max}, matcher={self.matcher}, task-filter={self.task_filter}}}"
+
 
 # -- GROUP_BY (round robin) --------------------------------------------------------------
 
@@ -702,7 +710,7 @@ class _RoundRobinRule(PlacementRule):
         return cls(d.get(cls.COUNT_KEY), _m(d))
 
     def __repr__(self):
-        return f"{type(self).__name__}{{{self.COUNT_KEY}={self.distinct_key_count}, task-filter={self.task_filter}}}"
+        return f"{type(self).__name__}{{{self.COUNT_KEY}={_opt(self.distinct_key_count)}, task-filter={self.task_filter}}}"
 
 
 @_rule
@@ -779,6 +787,10 @@ class RoundRobinByAttributeRule(_RoundRobinRule):
     @classmethod
     def from_dict(cls, d):
         return cls(d.get("name"), d.get(cls.COUNT_KEY), _m(d))
+
+    def __repr__(self):
+        return (f"RoundRobinByAttributeRule{{attribute={self.attribute_name}, "
+                f"attribute-count={_opt(self.distinct_key_count)}, task-filter={self.task_filter}}}")
 
 
 # -- task type affinity ------------------------------------------------------------------
