@@ -42,7 +42,8 @@ PROFILES = {
     "reference": {"SDK_EVENT_DRIVEN": "false", "SDK_OFFER_HOLD_S": "0", "SDK_OFFER_WAIT_S": "5",
                   "SDK_REVIVE_INTERVAL_S": "5", "SDK_REVIVE_BURST_INTERVAL_S": "5",
                   "SDK_RESERVATION_GC_ALL_OFFERS": "false",
-                  "SDK_FAST_UNSUPPRESS": "false", "SDK_MERGE_AGENT_OFFERS": "false"},
+                  "SDK_FAST_UNSUPPRESS": "false", "SDK_MERGE_AGENT_OFFERS": "false",
+                  "SDK_LAUNCH_RECONCILE_S": "0", "SDK_UNKNOWN_AS_LOST": "false"},
 }
 
 

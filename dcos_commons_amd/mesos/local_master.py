@@ -15,8 +15,11 @@ the SDK's timing and correctness depend on:
   task has a check, then ``exit_code`` once the readiness check passes, honouring
   ``delay_seconds``) -> terminal; KILL -> KILLED; executor resources are released when its last
   task ends; GPUs are assigned by device index (``HIP_VISIBLE_DEVICES`` for the task);
-* **reconciliation** (implicit and explicit), **teardown**, **agent loss** and fault injection
-  (``fail_task``, ``lose_agent``) for recovery/MTTR measurements.
+* **reconciliation** (implicit and explicit; an unknown task answers TASK_UNKNOWN to a
+  partition-aware framework, TASK_LOST otherwise), **teardown**, and fault injection for
+  recovery/MTTR measurements: ``fail_task``, ``send_status``, ``lose_agent`` /
+  ``reconnect_agent`` (partition and return), ``gone_by_operator``, ``forget_task``,
+  ``rescind_offers`` and ``drop_next_accepts`` (lost ACCEPT).
 
 All state is owned by one dispatcher thread (an actor): driver calls and test hooks enqueue
 actions, and scheduler callbacks are delivered from that thread in order.
@@ -238,6 +241,9 @@ class LocalMaster:
         self._thread = threading.Thread(target=self._run, name="LocalMaster", daemon=True)
         self._listeners: List[Callable[[str, P.TaskStatus], None]] = []
         self.accept_calls = 0
+        self.dropped_accepts = 0
+        self._drop_accepts = 0
+        self._drop_rescind_s = 0.5
         self.operations: List[Tuple[str, int]] = []  # (agent id, operation type) in applied order
         self._thread.start()
         self._schedule(self.allocation_interval_s, self._periodic_allocate)
@@ -325,6 +331,65 @@ class LocalMaster:
         def do():
             t = self._find_task(task_id)
             self._update(t, state, **fields)
+        self.call(do)
+
+    # -- fault injection (kill/lost/unreachable/gone task, agent loss and return,
+    #    offer rescind, dropped ACCEPT) ---------------------------------------------------
+    def rescind_offers(self, agent_id: Optional[str] = None) -> int:
+        """Rescind every outstanding offer (of one agent); returns how many were rescinded."""
+        def do():
+            oids = [o.id for o in self.offers.values() if agent_id is None or o.agent_id == agent_id]
+            for oid in oids:
+                self._rescind(oid)
+            return len(oids)
+        return self.call(do)
+
+    def drop_next_accepts(self, n: int = 1, rescind_after_s: float = 0.5) -> None:
+        """The next ``n`` ACCEPT calls are lost in transit: nothing is applied and the scheduler
+        hears nothing. The offers stay outstanding until the master's offer timeout rescinds them
+        (``rescind_after_s``), as a real master would after a lost message."""
+        def do():
+            self._drop_accepts += n
+            self._drop_rescind_s = rescind_after_s
+        self.call(do)
+
+    def gone_by_operator(self, agent_id: str) -> None:
+        """The operator marks an agent GONE: its tasks report TASK_GONE_BY_OPERATOR and the agent
+        (with its reservations) is removed for good."""
+        def do():
+            a = self.agents[agent_id]
+            a.active = False
+            for oid in [o.id for o in self.offers.values() if o.agent_id == agent_id]:
+                self._rescind(oid)
+            for t in list(a.tasks.values()):
+                if t.status.state not in TERMINAL:
+                    self._update(t, P.TASK_GONE_BY_OPERATOR, source=P.TaskStatus.SOURCE_MASTER,
+                                 reason=P.TaskStatus.REASON_AGENT_REMOVED, message="Agent marked gone by operator")
+            self.agents.pop(agent_id, None)
+        self.call(do)
+
+    def reconnect_agent(self, agent_id: str) -> None:
+        """A partitioned agent (``lose_agent``) re-registers: tasks that were UNREACHABLE and
+        are still alive on it report RUNNING again (Mesos' partition-aware re-registration)."""
+        def do():
+            a = self.agents[agent_id]
+            a.active = True
+            for t in list(a.tasks.values()):
+                if t.status.state == P.TASK_UNREACHABLE:
+                    self._update(t, P.TASK_RUNNING, source=P.TaskStatus.SOURCE_MASTER,
+                                 message="Agent re-registered")
+            self._allocate()
+        self.call(do)
+
+    def forget_task(self, task_id: str) -> None:
+        """The master loses all knowledge of a task (e.g. agent wiped while the scheduler was
+        down): no status is sent; reconciliation of it answers TASK_UNKNOWN / TASK_LOST."""
+        def do():
+            t = self._find_task(task_id)
+            if t is not None:
+                t.epoch += 1
+                self._release_task(t)
+                self.agents[t.agent_id].tasks.pop(task_id, None)
         self.call(do)
 
     def task_states(self, framework_id: Optional[str] = None) -> Dict[str, int]:
@@ -531,6 +596,12 @@ class LocalMaster:
     # -- ACCEPT -----------------------------------------------------------------------
     def _accept(self, fid: str, offer_ids: List[str], ops: List[P.Offer.Operation], refuse_s: float) -> None:
         self.accept_calls += 1
+        if self._drop_accepts > 0:
+            self._drop_accepts -= 1
+            self.dropped_accepts += 1
+            for oid in offer_ids:
+                self._schedule(self._drop_rescind_s, self._expire_offer, oid)
+            return
         fw = self._fw(fid)
         offers = [self.offers.get(oid) for oid in offer_ids]
         if fw is None or not offers or any(o is None or o.framework_id != fid for o in offers) or \
@@ -751,6 +822,17 @@ class LocalMaster:
             return
         if t.status.state in TERMINAL:
             return
+        if not self.agents[t.agent_id].active:
+            # Mesos cannot reach the agent: the kill is answered with the task's current
+            # (UNREACHABLE/LOST) state and nothing is released until the agent returns.
+            st = P.TaskStatus()
+            st.CopyFrom(t.status)
+            st.message = "Task is unreachable: cannot kill it now"
+            st.timestamp = time.time()
+            fw = self._fw(fid)
+            if fw is not None:
+                fw.driver._deliver(lambda s, d=fw.driver: s.status_update(d, st))
+            return
         self._update(t, P.TASK_KILLED, message="Task killed by scheduler")
 
     def _find_task(self, task_id: str) -> Optional[_Task]:
@@ -836,7 +918,8 @@ class LocalMaster:
                     c.reason = P.TaskStatus.REASON_RECONCILIATION
                     out.append(c)
                 else:
-                    st = P.TaskStatus(state=P.TASK_LOST, source=P.TaskStatus.SOURCE_MASTER,
+                    aware = any(c.type == P.FrameworkInfo.Capability.PARTITION_AWARE for c in fw.info.capabilities)
+                    st = P.TaskStatus(state=P.TASK_UNKNOWN if aware else P.TASK_LOST, source=P.TaskStatus.SOURCE_MASTER,
                                       reason=P.TaskStatus.REASON_RECONCILIATION, message="Reconciliation: task unknown",
                                       timestamp=time.time())
                     st.task_id.CopyFrom(s.task_id)

@@ -3,6 +3,8 @@
 Reference: sdk/.../scheduler/AbstractScheduler.java:36-262. ``get_client_status`` snapshots the
 candidate steps and updates the WorkSetTracker; ``offers`` refuses to launch until explicit
 reconciliation has finished; ``task_status`` stores the status and feeds the reconciler.
+Additions: launches are watched until their first status (``LaunchWatchdog``), and a
+reconciliation TASK_UNKNOWN is handled as TASK_LOST (``SDK_UNKNOWN_AS_LOST``).
 """
 from __future__ import annotations
 
@@ -10,14 +12,20 @@ import logging
 from typing import List, Optional
 
 from dcos_commons_amd.framework.process_exit import ProcessExit
+from dcos_commons_amd.mesos import protos as P
 from dcos_commons_amd.scheduler.mesos_event_client import (
     MesosEventClient,
     OfferResponse,
     TaskStatusResponse,
 )
-from dcos_commons_amd.scheduler.reconciliation import ExplicitReconciler, WorkSetTracker
+from dcos_commons_amd.scheduler.reconciliation import ExplicitReconciler, LaunchWatchdog, WorkSetTracker
 from dcos_commons_amd.state.state_store import StateStoreException
 from dcos_commons_amd.storage.persister import Reason
+
+
+def _cfg(scheduler_config, getter: str, default):
+    fn = getattr(scheduler_config, getter, None)
+    return fn() if callable(fn) else default
 
 
 class AbstractScheduler(MesosEventClient):
@@ -32,6 +40,8 @@ class AbstractScheduler(MesosEventClient):
         self.candidate_steps: List = []
         self.work_set_tracker: Optional[WorkSetTracker] = None
         self.reconciler: Optional[ExplicitReconciler] = None
+        self.launch_watchdog = LaunchWatchdog(_cfg(scheduler_config, "launch_reconcile_s", 0.0), namespace)
+        self.unknown_as_lost = _cfg(scheduler_config, "is_unknown_as_lost", False)
         self.logger = logging.getLogger(type(self).__module__ + (f"({namespace})" if namespace else ""))
 
     def customize_plans(self) -> None:
@@ -80,6 +90,7 @@ class AbstractScheduler(MesosEventClient):
             self.logger.error("WorkSetTracker is uninitialized (status requested before registration)")
             ProcessExit.exit(ProcessExit.ERROR, RuntimeError("WorkSetTracker uninitialized"))
         self.work_set_tracker.update_work_set(active)
+        self.launch_watchdog.poll()
         return self.get_status()
 
     def offers(self, offers) -> OfferResponse:
@@ -90,6 +101,17 @@ class AbstractScheduler(MesosEventClient):
         return self.process_offers(offers, self.candidate_steps)
 
     def task_status(self, status) -> TaskStatusResponse:
+        self.launch_watchdog.update(status)
+        if (self.unknown_as_lost and status.state == P.TASK_UNKNOWN
+                and status.reason == P.TaskStatus.REASON_RECONCILIATION):
+            # The master has no record of the task (it never got the launch, or the agent was
+            # wiped). The reference stores TASK_UNKNOWN and never recovers the task; treat it as
+            # lost so the recovery plan relaunches it.
+            lost = P.TaskStatus()
+            lost.CopyFrom(status)
+            lost.state = P.TASK_LOST
+            lost.message = f"Unknown to the master on reconciliation: {status.message}"
+            status = lost
         try:
             self.process_status_update(status)
             if self.reconciler is not None:

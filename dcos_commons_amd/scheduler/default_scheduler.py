@@ -15,6 +15,7 @@ from dcos_commons_amd.http import endpoint_utils
 from dcos_commons_amd.mesos import protos as P
 from dcos_commons_amd.offer.evaluate.offer_evaluator import OfferEvaluator
 from dcos_commons_amd.offer.history import OfferOutcomeTracker, OfferOutcomeTrackerV2
+from dcos_commons_amd.offer.recommendations import LaunchOfferRecommendation
 from dcos_commons_amd.offer.resources import get_all_resources, get_resource_id, get_resource_ids
 from dcos_commons_amd.scheduler.abstract_scheduler import AbstractScheduler
 from dcos_commons_amd.scheduler.decommission import DECOMMISSIONING_STATUS
@@ -29,11 +30,23 @@ from dcos_commons_amd.scheduler.plan.managers import DecommissionPlanManager
 from dcos_commons_amd.scheduler.plan.plan_scheduler import PlanScheduler
 from dcos_commons_amd.scheduler.plan.pod_instance_requirement import RecoveryType
 from dcos_commons_amd.scheduler.plan.status import Status
-from dcos_commons_amd.scheduler.recovery import RecoveryStep, is_permanently_failed
+from dcos_commons_amd.scheduler.recovery import RecoveryStep, is_permanently_failed, set_permanently_failed
 from dcos_commons_amd.scheduler.uninstall import UninstallRecorder
 from dcos_commons_amd.specification.specs import GoalState
 from dcos_commons_amd.state import state_store_utils
 from dcos_commons_amd.state.persistent_launch_recorder import PersistentLaunchRecorder
+
+
+_NEVER_LAUNCHED_STATES = (P.TASK_LOST, P.TASK_DROPPED)
+_NEVER_LAUNCHED_REASONS = (P.TaskStatus.REASON_RECONCILIATION, P.TaskStatus.REASON_INVALID_OFFERS)
+
+
+def _never_launched(prev: Optional[P.TaskStatus], status: P.TaskStatus) -> bool:
+    """The master reports a task it never saw (dropped ACCEPT, offer gone before the ACCEPT, or
+    forgotten) while our only record of it is the write-ahead STAGING status."""
+    return (prev is not None and prev.state == P.TASK_STAGING and prev.task_id.value == status.task_id.value
+            and status.source == P.TaskStatus.SOURCE_MASTER and status.state in _NEVER_LAUNCHED_STATES
+            and status.reason in _NEVER_LAUNCHED_REASONS)
 
 
 def _is_working(plan) -> bool:
@@ -167,6 +180,13 @@ class DefaultScheduler(AbstractScheduler):
             self.launch_recorder.record(recs)
             if self.decommission_recorder is not None:
                 self.decommission_recorder.record_decommission(recs)
+            if self.launch_watchdog.enabled:
+                for r in recs:
+                    if isinstance(r, LaunchOfferRecommendation):
+                        st = P.TaskStatus(state=P.TASK_STAGING)
+                        st.task_id.CopyFrom(r.task_info.task_id)
+                        st.agent_id.CopyFrom(r.task_info.agent_id)
+                        self.launch_watchdog.launched(st)
         except Exception:  # noqa: BLE001
             self.logger.exception("Failed to record offer operations, returning empty operations list")
             recs = []
@@ -202,7 +222,16 @@ class DefaultScheduler(AbstractScheduler):
         return UnexpectedResourcesResponse.processed(unexpected)
 
     def process_status_update(self, status: P.TaskStatus) -> None:
-        name = state_store_utils.fetch_task_info(self.state_store, status).name
+        info = state_store_utils.fetch_task_info(self.state_store, status)
+        name = info.name
+        if self.unknown_as_lost and _never_launched(self.state_store.fetch_status(name), status):
+            # The launch was recorded (write-ahead) but its ACCEPT never took effect, so the
+            # reservations in the stored TaskInfo do not exist and an in-place relaunch would
+            # wait for them forever. Mark it permanently failed: the step relaunches with a fresh
+            # footprint and anything that was reserved is garbage-collected as unexpected.
+            self.logger.warning("Launch of %s never reached the master (%s, %s): relaunching with new reservations",
+                                name, P.TaskState.Name(status.state), P.TaskStatus.Reason.Name(status.reason))
+            set_permanently_failed(self.state_store, [info])
         self.state_store.store_status(name, status)
         for pm in self.plan_coordinator.get_plan_managers():
             pm.update(status)

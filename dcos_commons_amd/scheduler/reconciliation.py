@@ -2,6 +2,7 @@
 
 Reference: sdk/.../scheduler/ExplicitReconciler.java:36-251 (backoff 4 s -> x2 -> 30 s; offers are
 refused until every non-terminal task has been reconciled) and WorkSetTracker.java:21-136.
+``LaunchWatchdog`` has no reference counterpart (see its docstring).
 """
 from __future__ import annotations
 
@@ -80,6 +81,69 @@ class ExplicitReconciler:
     def remaining(self) -> Set[str]:
         with self._r:
             return set(self._unreconciled)
+
+
+class LaunchWatchdog:
+    """Reconciles launches that never left TASK_STAGING.
+
+    The launch is recorded (TaskInfo + a synthetic STAGING status) before the ACCEPT goes out
+    (write-ahead, DefaultScheduler.java:455). If that ACCEPT is lost, the master never hears of
+    the task and nothing ever updates it: the reference leaves the step STARTING until a
+    scheduler restart re-runs explicit reconciliation. Here every recorded launch is watched;
+    one still without a status after ``timeout_s`` is reconciled explicitly (the master answers
+    TASK_UNKNOWN/TASK_LOST for a task it never saw, which sends the step back to PENDING), with
+    the usual x2 backoff up to ``MAX_BACKOFF_MS``. ``timeout_s <= 0`` disables the watchdog
+    (reference behaviour).
+    """
+
+    def __init__(self, timeout_s: float, namespace: Optional[str] = None,
+                 clock: Callable[[], float] = time.monotonic):
+        self.timeout_s = timeout_s
+        self.clock = clock
+        self.logger = logging.getLogger(__name__ + (f"({namespace})" if namespace else ""))
+        self._lock = new_rw_lock("LaunchWatchdog").write_lock
+        # task id -> (next deadline, current backoff, staging status)
+        self._watched: Dict[str, tuple] = {}
+
+    @property
+    def enabled(self) -> bool:
+        return self.timeout_s > 0
+
+    def launched(self, status: P.TaskStatus) -> None:
+        if not self.enabled or not status.task_id.value:
+            return
+        with self._lock:
+            self._watched[status.task_id.value] = (self.clock() + self.timeout_s, self.timeout_s, status)
+
+    def update(self, status: P.TaskStatus) -> None:
+        if status.state == P.TASK_STAGING and status.source != P.TaskStatus.SOURCE_MASTER:
+            return
+        with self._lock:
+            self._watched.pop(status.task_id.value, None)
+
+    def watched(self) -> Set[str]:
+        with self._lock:
+            return set(self._watched)
+
+    def poll(self) -> int:
+        """Reconcile every overdue launch; returns how many were sent."""
+        if not self._watched:
+            return 0
+        now = self.clock()
+        due = []
+        with self._lock:
+            for tid, (deadline, backoff, st) in list(self._watched.items()):
+                if now >= deadline:
+                    nb = min(backoff * MULTIPLIER, MAX_BACKOFF_MS / 1000.0)
+                    self._watched[tid] = (now + nb, nb, st)
+                    due.append(st)
+        if due:
+            self.logger.warning("Reconciling %d launch(es) still STAGING after %.1fs: %s", len(due), self.timeout_s,
+                                [s.task_id.value for s in due])
+            d = driver.get_instance()
+            if d is not None:
+                d.reconcile_tasks(due)
+        return len(due)
 
 
 class WorkSetTracker:

@@ -261,6 +261,20 @@ class SchedulerConfig:
         """First REVIVE after a SUPPRESS skips the burst spacing (reference: never)."""
         return self.env.get_optional_boolean("SDK_FAST_UNSUPPRESS", True)
 
+    def launch_reconcile_s(self) -> float:
+        """Explicitly reconcile a launch that still has no status after this many seconds, e.g.
+        because its ACCEPT was lost (0 = reference behaviour: wait for the next scheduler
+        restart)."""
+        return self.env.get_optional_double("SDK_LAUNCH_RECONCILE_S", 30.0)
+
+    def is_unknown_as_lost(self) -> bool:
+        """Trust the master's "never heard of this task": a reconciliation TASK_UNKNOWN is handled as
+        TASK_LOST so the task is recovered, and a launch the master reports LOST/DROPPED while our
+        only record is the write-ahead STAGING status is relaunched with fresh reservations
+        (reference: the UNKNOWN status is stored and never recovered, and such a launch waits
+        forever for reservations that were never made)."""
+        return self.env.get_optional_boolean("SDK_UNKNOWN_AS_LOST", True)
+
     def implicit_reconcile_delay_s(self) -> float:
         return self.implicit_reconcile_delay_ms() / 1000.0
 

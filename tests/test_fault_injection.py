@@ -1,0 +1,215 @@
+"""Fault injection against the live scheduler on the in-process master.
+
+The reference injects faults only in its DC/OS integration tests (pkill, iptables partitions,
+agent shutdown, master/ZK kills: testing/sdk_cmd.py, sdk_agents.py, helloworld/tests/
+test_zzzrecovery.py) and in simulation ticks. Here the fake master's injectors drive the same
+situations in-process: a lost ACCEPT, offer rescinds mid-deploy, an agent partition that heals,
+an agent marked gone by the operator, a scheduler crash + restart (resume from the persister),
+and a task the master forgot while the scheduler was down.
+"""
+import os
+import threading
+import time
+
+from dcos_commons_amd.mesos import protos as P
+from dcos_commons_amd.mesos.local_master import AgentSpec, LocalMaster, LocalSchedulerDriver
+from dcos_commons_amd.scheduler.scheduler_builder import SchedulerBuilder
+from dcos_commons_amd.scheduler.scheduler_config import SchedulerConfig
+from dcos_commons_amd.scheduler.scheduler_runner import SchedulerRunner
+from dcos_commons_amd.specification.yaml.mappers import ServiceSpecGenerator
+from dcos_commons_amd.specification.yaml.raw import RawServiceSpec
+from dcos_commons_amd.storage.mem_persister import MemPersister
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SPECS = os.path.join(ROOT, "frameworks", "helloworld", "specs")
+ENV = dict(FRAMEWORK_NAME="hello-world", FRAMEWORK_PRINCIPAL="hw-principal", FRAMEWORK_USER="nobody",
+           HELLO_COUNT="2", HELLO_PLACEMENT='[["hostname", "UNIQUE"]]', HELLO_CPUS="0.1", HELLO_MEM="252",
+           HELLO_DISK="25", SLEEP_DURATION="1000", WORLD_COUNT="2", WORLD_PLACEMENT='[["hostname", "UNIQUE"]]',
+           WORLD_CPUS="0.2", WORLD_MEM="512", WORLD_DISK="25", WORLD_READINESS_CHECK_INTERVAL="5",
+           WORLD_READINESS_CHECK_DELAY="0", WORLD_READINESS_CHECK_TIMEOUT="10")
+
+
+class Chaos:
+    def __init__(self, agents=3, **cfg):
+        overrides = {"PORT_API": "0", "SDK_OFFER_WAIT_S": "0.2", "SDK_LAUNCH_RECONCILE_S": "0.3"}
+        overrides.update(cfg)
+        self.cfg = SchedulerConfig.for_testing(**overrides)
+        self.raw = RawServiceSpec.new_builder(os.path.join(SPECS, "svc.yml")).set_env(ENV).build()
+        self.spec = ServiceSpecGenerator(self.raw, self.cfg, SPECS, ENV).build()
+        self.master = LocalMaster(allocation_interval_s=0.05)
+        self.agent_ids = [self.master.add_agent(AgentSpec(hostname=f"host-{i}", cpus=4, mem=8192, disk=20000))
+                          for i in range(agents)]
+        self.persister = MemPersister()
+        self.runner = None
+
+    def start(self):
+        self.runner = SchedulerRunner(SchedulerBuilder(self.spec, self.cfg, self.persister).set_plans_from(self.raw),
+                                      driver_factory=lambda s, i: LocalSchedulerDriver(self.master, s, i))
+        self.runner.run(block=False)
+        self.api = self.runner.framework_runner.api_server.router
+        self.store = self.runner.scheduler.state_store
+        return self
+
+    def crash(self):
+        """Scheduler process dies: the driver fails over (tasks keep running), nothing else."""
+        self.runner.stop()
+        self.runner = None
+
+    def __enter__(self):
+        return self.start()
+
+    def __exit__(self, *exc):
+        if self.runner is not None:
+            self.runner.stop()
+        self.master.shutdown()
+
+    def wait(self, pred, timeout=20.0, what="condition"):
+        t0 = time.time()
+        while time.time() - t0 < timeout:
+            if pred():
+                return
+            time.sleep(0.005)
+        raise AssertionError(f"{what} not reached in {timeout}s")
+
+    def plan_code(self, name):
+        return self.api.get(f"/v1/plans/{name}").status
+
+    def wait_plan(self, name, timeout=20.0):
+        self.wait(lambda: self.plan_code(name) == 200, timeout, f"plan {name} COMPLETE")
+
+    def task_id(self, name):
+        t = self.store.fetch_task(name)
+        return t.task_id.value if t is not None else None
+
+    def state(self, name):
+        s = self.store.fetch_status(name)
+        return s.state if s is not None else None
+
+    def agent_of(self, name):
+        return self.store.fetch_task(name).agent_id.value
+
+    def running_ids(self):
+        return {tid for tid, st in self.master.task_states().items() if st == P.TASK_RUNNING}
+
+
+def test_lost_accept_is_reconciled_and_relaunched():
+    with Chaos() as c:
+        c.master.drop_next_accepts(1)
+        c.wait_plan("deploy", 30)
+        assert c.master.dropped_accepts == 1
+        # every stored task is the one the master is running
+        for name in ("hello-0-server", "hello-1-server", "world-0-server", "world-1-server"):
+            assert c.task_id(name) in c.running_ids()
+        assert c.runner.scheduler.launch_watchdog.watched() == set()
+
+
+def test_lost_accept_stalls_without_the_watchdog():
+    """Reference behaviour: a lost ACCEPT leaves its step STARTING until a restart."""
+    with Chaos(SDK_LAUNCH_RECONCILE_S="0") as c:
+        c.master.drop_next_accepts(1)
+        time.sleep(1.5)
+        assert c.plan_code("deploy") == 202
+        assert c.state("hello-0-server") == P.TASK_STAGING
+        c.crash()
+        c.start()                        # explicit reconciliation at re-registration recovers it
+        c.wait_plan("deploy", 30)
+
+
+def test_offer_rescinds_during_deploy():
+    with Chaos() as c:
+        stop = threading.Event()
+
+        def rescinder():
+            while not stop.is_set():
+                c.master.rescind_offers()
+                time.sleep(0.03)
+        t = threading.Thread(target=rescinder, daemon=True)
+        t.start()
+        try:
+            time.sleep(0.3)
+        finally:
+            stop.set()
+            t.join()
+        c.wait_plan("deploy", 30)
+        assert len(c.running_ids()) == 4
+
+
+def _volume_ids(c, name):
+    return sorted(r.disk.persistence.id for r in c.store.fetch_task(name).resources if r.disk.persistence.id)
+
+
+def test_agent_partition_heals_and_pod_relaunches_in_place():
+    """UNREACHABLE starts a TRANSIENT recovery; its kill cannot reach the agent (the master
+    answers UNREACHABLE and keeps the resources). When the agent returns, the recovery kills
+    the stale task and relaunches the pod in place: same agent, same persistent volume."""
+    with Chaos() as c:
+        c.wait_plan("deploy")
+        tid = c.task_id("hello-0-server")
+        aid = c.agent_of("hello-0-server")
+        vols = _volume_ids(c, "hello-0-server")
+        c.master.lose_agent(aid)
+        c.wait(lambda: c.state("hello-0-server") == P.TASK_UNREACHABLE, what="UNREACHABLE")
+        c.wait(lambda: c.plan_code("recovery") == 202, what="recovery in progress")
+        time.sleep(0.3)
+        assert c.task_id("hello-0-server") == tid          # nothing can move while partitioned
+        c.master.reconnect_agent(aid)
+        c.wait(lambda: c.task_id("hello-0-server") != tid and c.state("hello-0-server") == P.TASK_RUNNING,
+               what="relaunched in place")
+        c.wait_plan("recovery")
+        assert c.agent_of("hello-0-server") == aid
+        assert _volume_ids(c, "hello-0-server") == vols
+        assert c.master.task_states()[tid] == P.TASK_KILLED
+
+
+def test_agent_gone_by_operator_is_replaced_elsewhere():
+    with Chaos(agents=4) as c:
+        c.wait_plan("deploy")
+        old_agent = c.agent_of("world-0-server")
+        old_tid = c.task_id("world-0-server")
+        c.master.gone_by_operator(old_agent)
+        c.wait(lambda: c.task_id("world-0-server") != old_tid and c.state("world-0-server") == P.TASK_RUNNING,
+               what="world-0 replaced")
+        c.wait_plan("recovery")
+        assert c.agent_of("world-0-server") != old_agent
+        assert c.task_id("world-0-server") in c.running_ids()
+
+
+def test_scheduler_restart_resumes_without_relaunch():
+    with Chaos() as c:
+        c.wait_plan("deploy")
+        before = {n: c.task_id(n) for n in ("hello-0-server", "hello-1-server", "world-0-server", "world-1-server")}
+        launches = c.master.accept_calls
+        c.crash()
+        c.start()
+        c.wait_plan("deploy")
+        after = {n: c.task_id(n) for n in before}
+        assert after == before
+        time.sleep(0.3)
+        # re-registration reconciles; nothing was relaunched
+        assert set(before.values()) <= c.running_ids()
+        assert c.master.accept_calls - launches <= 1   # at most an idle reservation-GC accept
+
+
+def test_task_forgotten_while_scheduler_down_is_recovered():
+    with Chaos() as c:
+        c.wait_plan("deploy")
+        tid = c.task_id("world-1-server")
+        c.crash()
+        c.master.forget_task(tid)
+        c.start()
+        c.wait(lambda: c.task_id("world-1-server") != tid and c.state("world-1-server") == P.TASK_RUNNING,
+               timeout=30, what="world-1 relaunched")
+        c.wait_plan("recovery", 30)
+
+
+def test_task_forgotten_reference_behaviour_never_recovers():
+    """With SDK_UNKNOWN_AS_LOST=false the TASK_UNKNOWN reply is stored and nothing recovers it."""
+    with Chaos(SDK_UNKNOWN_AS_LOST="false") as c:
+        c.wait_plan("deploy")
+        tid = c.task_id("world-1-server")
+        c.crash()
+        c.master.forget_task(tid)
+        c.start()
+        c.wait(lambda: c.state("world-1-server") == P.TASK_UNKNOWN, what="TASK_UNKNOWN stored")
+        time.sleep(0.5)
+        assert c.task_id("world-1-server") == tid
