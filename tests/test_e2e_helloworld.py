@@ -67,13 +67,13 @@ class Cluster:
             self.http_master.stop()
         self.master.shutdown()
 
-    def wait(self, pred, timeout=20.0):
+    def wait(self, pred, timeout=20.0, what="condition"):
         t0 = time.time()
         while time.time() - t0 < timeout:
             if pred():
                 return
             time.sleep(0.005)
-        raise AssertionError("condition not reached")
+        raise AssertionError(f"{what} not reached in {timeout}s")
 
     def wait_plan(self, name, code=200, timeout=20.0):
         self.wait(lambda: self.api.get(f"/v1/plans/{name}").status == code, timeout)
