@@ -186,6 +186,42 @@ int hdfs_plugin(const std::vector<std::string>& hdfs_args) {
   return WIFEXITED(status) ? WEXITSTATUS(status) : 1;
 }
 
+// Reference cli/queries/plan.go checkPlansResponse: a scheduler 404 means the plan/phase/step is
+// unknown, 208 that the command is a no-op. Returns false (after printing the error) for those.
+bool plan_response(const sdk::HttpResponse& r) {
+  if (r.status == 404) {
+    bool scheduler_404 = r.body == "Element not found" ||
+                         (r.body.size() > 10 && r.body.compare(r.body.size() - 10, 10, " not found") == 0);
+    if (scheduler_404) {
+      std::cerr << "Plan, phase, and/or step does not exist" << std::endl;
+      return false;
+    }
+  }
+  if (r.status == 208) {
+    std::cerr << "Cannot execute command. Command has already been issued or the plan has completed" << std::endl;
+    return false;
+  }
+  if (r.status < 200 || r.status >= 300) {
+    emit(r);
+    return false;
+  }
+  return true;
+}
+
+// A plan command answered {"message": "..."} on success; anything else "could not be" done.
+int plan_command(Ctx& c, const std::string& path, const std::string& target, const std::string& verb) {
+  auto r = call(c, "POST", path);
+  if (!plan_response(r)) return 1;
+  bool valid = false;
+  try {
+    auto j = sdk::Json::parse(r.body);
+    valid = j.is_object() && j["message"].is_string() && !j["message"].str().empty();
+  } catch (...) {
+  }
+  std::cout << target << (valid ? " has been " : " could not be ") << verb << "." << std::endl;
+  return 0;
+}
+
 int plan_cmd(Ctx& c, const std::vector<std::string>& a) {
   std::string cmd = arg(a, 0);
   if (cmd == "list") return emit(call(c, "GET", "/plans"));
@@ -213,15 +249,24 @@ int plan_cmd(Ctx& c, const std::vector<std::string>& a) {
         params.set(kv.substr(0, eq), sdk::Json(kv.substr(eq + 1)));
       }
     }
-    return emit(call(c, "POST", p + "/start", params.dump()));
+    auto r = call(c, "POST", p + "/start", params.dump());
+    return plan_response(r) ? emit(r) : 1;
   }
-  if (cmd == "stop") return emit(call(c, "POST", p + "/stop"));
-  if (cmd == "pause") return emit(call(c, "POST", p + "/interrupt" + query({{"phase", arg(a, 2)}})));
-  if (cmd == "resume") return emit(call(c, "POST", p + "/continue" + query({{"phase", arg(a, 2)}})));
+  if (cmd == "stop") {
+    auto r = call(c, "POST", p + "/stop");
+    return plan_response(r) ? emit(r) : 1;
+  }
+  std::string phase = arg(a, 2), step = arg(a, 3);
+  std::string q = "\"" + plan + "\" plan";
+  std::string target = step.empty() ? (phase.empty() ? q : q + ": phase \"" + phase + "\"")
+                                    : q + ": step \"" + step + "\" in phase \"" + phase + "\"";
+  if (cmd == "pause") return plan_command(c, p + "/interrupt" + query({{"phase", phase}}), target, "paused");
+  if (cmd == "resume") return plan_command(c, p + "/continue" + query({{"phase", phase}}), target, "resumed");
   if (cmd == "force-restart")
-    return emit(call(c, "POST", p + "/restart" + query({{"phase", arg(a, 2)}, {"step", arg(a, 3)}})));
+    return plan_command(c, p + "/restart" + query({{"phase", phase}, {"step", step}}), target, "restarted");
   if (cmd == "force-complete")
-    return emit(call(c, "POST", p + "/forceComplete" + query({{"phase", arg(a, 2)}, {"step", arg(a, 3)}})));
+    return plan_command(c, p + "/forceComplete" + query({{"phase", phase}, {"step", step}}),
+                        q + ": step \"" + step + "\" in phase \"" + phase + "\"", "forced to complete");
   usage();
   return 1;
 }

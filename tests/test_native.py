@@ -105,8 +105,10 @@ def test_cli_against_live_scheduler(tools):
         assert rc == 0 and out.splitlines()[0] == "hello-world" and "hello-0-server (RUNNING)" in out
         rc, out, _ = cli("pod", "status", "world-1")
         assert rc == 0 and out.splitlines() == ["world-1", "└─ world-1-server (RUNNING)"]
-        rc, out, _ = cli("plan", "pause", "deploy")
-        assert rc == 0 and "already been reported" in out
+        rc, _, err = cli("plan", "pause", "deploy")
+        assert rc == 1 and "Command has already been issued or the plan has completed" in err
+        rc, _, err = cli("plan", "resume", "deploy", "nope")
+        assert rc == 1 and err.strip() == "Plan, phase, and/or step does not exist"
         rc, _, err = cli("pod", "info", "nope-9")
         assert rc == 2 and "404" in err
         rc, out, _ = cli("debug", "state", "framework_id")
