@@ -75,7 +75,7 @@ def _any(status: Status, statuses) -> bool:
 
 
 def get_aggregate_status(parent_name: str, child_statuses: List[Status], candidate_statuses: List[Status],
-                         errors: List[str], is_interrupted: bool) -> Status:
+                         errors: List[str], is_interrupted: bool, log_unexpected: bool = True) -> Status:
     if errors or _any(Status.ERROR, child_statuses):
         return Status.ERROR
     if _all(Status.COMPLETE, child_statuses):
@@ -104,8 +104,9 @@ def get_aggregate_status(parent_name: str, child_statuses: List[Status], candida
         return Status.STARTING
     if _any(Status.STARTED, candidate_statuses):
         return Status.STARTED
-    LOGGER.warning("(%s status=ERROR) Unexpected state. Children: %s Candidates: %s",
-                   parent_name, child_statuses, candidate_statuses)
+    if log_unexpected:
+        LOGGER.warning("(%s status=ERROR) Unexpected state. Children: %s Candidates: %s",
+                       parent_name, child_statuses, candidate_statuses)
     return Status.ERROR
 
 
@@ -218,12 +219,25 @@ class ParentElement(Element):
             out.extend(c.get_errors())
         return out
 
+    # Children change status on other threads (status updates, the offer loop) while the
+    # aggregate is computed: the child statuses, the strategy's candidates and the candidates'
+    # statuses are three separate reads, and a step completing between them yields a combination
+    # no rule covers (e.g. children [STARTED], candidates [COMPLETE]). Such a torn read is retried
+    # instead of being reported as ERROR; a persistent one still is.
+    _TORN_READ_RETRIES = 3
+
     def get_status(self) -> Status:
         children = self.get_children()
-        child_statuses = [c.get_status() for c in children]
-        candidate_statuses = [c.get_status() for c in self.get_strategy().get_candidates(children, [])]
-        return get_aggregate_status(self.get_name(), child_statuses, candidate_statuses, self.get_errors(),
-                                    self.is_interrupted())
+        errors = self.get_errors()
+        for attempt in range(self._TORN_READ_RETRIES + 1):
+            child_statuses = [c.get_status() for c in children]
+            candidate_statuses = [c.get_status() for c in self.get_strategy().get_candidates(children, [])]
+            last = attempt == self._TORN_READ_RETRIES
+            st = get_aggregate_status(self.get_name(), child_statuses, candidate_statuses, errors,
+                                      self.is_interrupted(), log_unexpected=last)
+            if st != Status.ERROR or errors or Status.ERROR in child_statuses or last:
+                return st
+        return st
 
 
 class Step(Element):

@@ -84,6 +84,11 @@ class _OrderTracker:
         stack = _held_stack()
         if not stack or self.lock_id in stack:
             return
+        # Fast path: every held -> this edge is already known (and was cycle-checked when it was
+        # added). Set membership reads are atomic under the GIL, so no graph lock is needed.
+        lid = self.lock_id
+        if all(lid in _edges.get(held, ()) for held in stack):
+            return
         with _graph_lock:
             for held in stack:
                 if self.lock_id in _edges.get(held, ()):
@@ -170,6 +175,7 @@ class CycleDetectingRWLock:
         self._writer: Optional[int] = None
         self._write_depth = 0
         self._tracker = _OrderTracker(name, check)
+        self._waiting = 0  # threads blocked in _cond.wait(): release only notifies when > 0
         self.read_lock = _RWView(self, False)
         self.write_lock = _RWView(self, True)
 
@@ -178,7 +184,11 @@ class CycleDetectingRWLock:
         me = threading.get_ident()
         with self._cond:
             while self._writer is not None and self._writer != me:
-                self._cond.wait()
+                self._waiting += 1
+                try:
+                    self._cond.wait()
+                finally:
+                    self._waiting -= 1
             self._readers[me] = self._readers.get(me, 0) + 1
         self._tracker.acquired()
 
@@ -191,7 +201,8 @@ class CycleDetectingRWLock:
                 self._readers.pop(me, None)
             else:
                 self._readers[me] = n
-            self._cond.notify_all()
+            if self._waiting:
+                self._cond.notify_all()
 
     def acquire_write(self) -> None:
         self._tracker.before_acquire()
@@ -201,7 +212,11 @@ class CycleDetectingRWLock:
                 self._write_depth += 1
             else:
                 while self._writer is not None or any(t != me for t in self._readers):
-                    self._cond.wait()
+                    self._waiting += 1
+                    try:
+                        self._cond.wait()
+                    finally:
+                        self._waiting -= 1
                 self._writer = me
                 self._write_depth = 1
         self._tracker.acquired()
@@ -212,7 +227,8 @@ class CycleDetectingRWLock:
             self._write_depth -= 1
             if self._write_depth == 0:
                 self._writer = None
-            self._cond.notify_all()
+            if self._waiting:
+                self._cond.notify_all()
 
 
 def deadlock_checks_enabled() -> bool:
