@@ -35,6 +35,9 @@ def parse_args(argv=None):
     ap.add_argument("--allocation-interval", type=float, default=1.0,
                     help="fake Mesos master allocation interval (Mesos default 1 s)")
     ap.add_argument("--no-gpu-probe", action="store_true", help="synthetic readiness (no HIP probe)")
+    ap.add_argument("--dist-backend", default="auto", choices=["auto", "nccl", "gloo"],
+                    help="torch.distributed backend (auto: nccl=RCCL on GPUs, gloo on CPU; gloo lets several "
+                         "ranks share one GPU for a rehearsal)")
     ap.add_argument("--verbose", action="store_true")
     return ap.parse_args(argv)
 
@@ -54,9 +57,12 @@ def main(argv=None) -> int:
     if world > 1:
         import torch.distributed as dist
 
-        backend = "nccl" if torch.cuda.is_available() else "gloo"
+        backend = args.dist_backend if args.dist_backend != "auto" else (
+            "nccl" if torch.cuda.is_available() else "gloo")
+        args.dist_backend = backend
         if torch.cuda.is_available():
-            torch.cuda.set_device(local_rank)
+            # one rank per GPU; more ranks than GPUs share them round-robin (gloo rehearsals)
+            torch.cuda.set_device(local_rank % torch.cuda.device_count())
         dist.init_process_group(backend=backend)
 
     from dcos_commons_amd.benchmarks.runner import run_bench

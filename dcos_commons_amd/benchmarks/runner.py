@@ -105,19 +105,23 @@ def _run_distributed(args, rank, world, local_rank, use_gpu, dist):
                                             master_addr)
         port_box[0] = server.port
     dist.broadcast_object_list(port_box, src=0)
+    n_dev = torch.cuda.device_count() if torch.cuda.is_available() else 1
+    device = local_rank % max(n_dev, 1)
     local_check = gpu_check_runner() if use_gpu else None
+    # collectives run on the GPU under RCCL, on the host under gloo
+    coll_dev = "cuda" if torch.cuda.is_available() and getattr(args, "dist_backend", "nccl") == "nccl" else "cpu"
 
     def check(msg):
         if local_check is None:
             return True, "synthetic"
-        ok = local_check(None, [local_rank])
+        ok = local_check(None, [device])
         return ok, "probe"
 
     if rank != 0:
-        info = {"rank": rank, "hostname": f"{socket.gethostname()}-gpu{local_rank}", "devices": [local_rank]}
+        info = {"rank": rank, "hostname": f"{socket.gethostname()}-gpu{local_rank}", "devices": [device]}
         agent_link.run_agent(master_addr, port_box[0], info, check, on_barrier=lambda: (_sync(), dist.barrier()))
         # final MAX reduction of the timed region (rank 0 drives it)
-        t = torch.zeros(1, dtype=torch.float64, device="cuda" if torch.cuda.is_available() else "cpu")
+        t = torch.zeros(1, dtype=torch.float64, device=coll_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return {}
 
@@ -144,6 +148,6 @@ def _run_distributed(args, rank, world, local_rank, use_gpu, dist):
     barrier()
     elapsed = time.perf_counter() - t0
     server.close()
-    t = torch.tensor([elapsed], dtype=torch.float64, device="cuda" if torch.cuda.is_available() else "cpu")
+    t = torch.tensor([elapsed], dtype=torch.float64, device=coll_dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return _summary(args, world, cycles, float(t.item()), use_gpu, f"agents{world}-ranks{world}")
