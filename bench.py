@@ -38,6 +38,8 @@ def parse_args(argv=None):
     ap.add_argument("--dist-backend", default="auto", choices=["auto", "nccl", "gloo"],
                     help="torch.distributed backend (auto: nccl=RCCL on GPUs, gloo on CPU; gloo lets several "
                          "ranks share one GPU for a rehearsal)")
+    ap.add_argument("--sched-env", action="append", default=[], metavar="KEY=VALUE",
+                    help="scheduler flag override on top of --profile (A/B experiments)")
     ap.add_argument("--verbose", action="store_true")
     return ap.parse_args(argv)
 

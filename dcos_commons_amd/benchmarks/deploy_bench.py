@@ -43,7 +43,7 @@ PROFILES = {
                   "SDK_REVIVE_INTERVAL_S": "5", "SDK_REVIVE_BURST_INTERVAL_S": "5",
                   "SDK_RESERVATION_GC_ALL_OFFERS": "false",
                   "SDK_FAST_UNSUPPRESS": "false", "SDK_MERGE_AGENT_OFFERS": "false",
-                  "SDK_LAUNCH_RECONCILE_S": "0", "SDK_UNKNOWN_AS_LOST": "false"},
+                  "SDK_LAUNCH_RECONCILE_S": "0", "SDK_UNKNOWN_AS_LOST": "false", "SDK_STREAM_LAUNCHES": "false"},
 }
 
 
@@ -70,8 +70,10 @@ class DeployBench:
     def __init__(self, n_agents: int, profile: str = "mi355x", spec_file: str = "gpu.yml",
                  check_runner: Optional[Callable[[P.TaskInfo, List[int]], bool]] = None,
                  gpu_devices: Optional[List[int]] = None, allocation_interval_s: float = 1.0,
-                 timeout_s: float = 120.0, agent_runners: Optional[List[Callable]] = None):
+                 timeout_s: float = 120.0, agent_runners: Optional[List[Callable]] = None,
+                 extra_env: Optional[Dict[str, str]] = None):
         self.n = n_agents
+        self.extra_env = dict(extra_env or {})  # scheduler flag overrides on top of the profile
         self.profile = profile
         self.spec_file = spec_file
         self.check_runner = check_runner
@@ -133,6 +135,7 @@ class DeployBench:
         t_cycle = time.perf_counter()
         env = helloworld_env(self.n, 1, "amd-gpu-probe --readiness")
         overrides = dict(PROFILES[self.profile])
+        overrides.update(self.extra_env)
         overrides.update({"PORT_API": "0", "SDK_PERSISTER": "mem"})
         cfg = SchedulerConfig.for_testing(**overrides)
         path = os.path.join(SPECS, self.spec_file)

@@ -36,6 +36,10 @@ def _sync():
         torch.cuda.synchronize()
 
 
+def _sched_env(args) -> dict:
+    return dict(kv.split("=", 1) for kv in getattr(args, "sched_env", None) or [])
+
+
 def run_bench(args, rank: int, world: int, local_rank: int, use_gpu: bool, dist=None) -> dict:
     n = args.gpus if world == 1 else world
     if world > 1 and args.gpus != world:
@@ -67,7 +71,8 @@ def _summary(args, n, cycles, elapsed, use_gpu, parallelism):
         "config": {"model": "helloworld gpu.yml (gpus:1 per pod, hostname:UNIQUE, parallel deploy)",
                    "global_batch": n, "seq_len": 0, "parallelism": parallelism,
                    "pods": n, "agents": n, "profile": args.profile,
-                   "allocation_interval_s": args.allocation_interval},
+                   "allocation_interval_s": args.allocation_interval,
+                   **({"scheduler_overrides": _sched_env(args)} if _sched_env(args) else {})},
         "deploy_s": {"mean": round(value, 6), "min": round(min(deploy), 6), "max": round(max(deploy), 6)},
         "mttr_restart_s": {"mean": round(statistics.mean(restart), 6), "max": round(max(restart), 6)},
         "mttr_replace_s": {"mean": round(statistics.mean(replace), 6), "max": round(max(replace), 6)},
@@ -81,7 +86,7 @@ def _run_single(args, n, use_gpu):
     ndev = torch.cuda.device_count() if use_gpu else 1
     bench = DeployBench(n, profile=args.profile, check_runner=runner,
                         gpu_devices=[i % max(1, ndev) for i in range(n)],
-                        allocation_interval_s=args.allocation_interval)
+                        allocation_interval_s=args.allocation_interval, extra_env=_sched_env(args))
     for _ in range(args.warmup):
         bench.run_cycle()
     _sync()
@@ -132,7 +137,7 @@ def _run_distributed(args, rank, world, local_rank, use_gpu, dist):
 
     runners = [local_runner] + [r.run_check for r in remotes]
     bench = DeployBench(world, profile=args.profile, agent_runners=runners, gpu_devices=list(range(world)),
-                        allocation_interval_s=args.allocation_interval)
+                        allocation_interval_s=args.allocation_interval, extra_env=_sched_env(args))
     for _ in range(args.warmup):
         bench.run_cycle()
 

@@ -41,7 +41,8 @@ class FrameworkScheduler:
             event_driven=scheduler_config.is_event_driven() if scheduler_config is not None else False,
             gc_all_offers=scheduler_config.is_reservation_gc_on_all_offers() if scheduler_config is not None else False,
             fast_unsuppress=scheduler_config.is_fast_unsuppress() if scheduler_config is not None else False,
-            merge_agent_offers=scheduler_config.is_merge_agent_offers() if scheduler_config is not None else False)
+            merge_agent_offers=scheduler_config.is_merge_agent_offers() if scheduler_config is not None else False,
+            stream_launches=scheduler_config.is_stream_launches() if scheduler_config is not None else False)
         if implicit_reconciler is None:
             implicit_reconciler = ImplicitReconciler(
                 scheduler_config.implicit_reconcile_delay_s() if scheduler_config is not None else 0.0,

@@ -10,7 +10,10 @@ MI355X-build changes (all opt-in knobs, reference behaviour is the default of ea
   immediately instead of waiting out the 5 s offer poll (OfferProcessor.java:46);
 * **bounded offer holding** -- while the service is WORKING, unused offers can be held for up to
   ``hold_s`` and re-evaluated as plans advance instead of being declined for an hour and
-  re-obtained through a (rate-limited) REVIVE. ``hold_s=0`` is the reference behaviour.
+  re-obtained through a (rate-limited) REVIVE. ``hold_s=0`` is the reference behaviour;
+* **launch streaming** -- each matched step is recorded and ACCEPTed before the next step is
+  evaluated (``stream_launches``), so a large parallel deploy starts its first pods while the
+  rest are still being matched. The reference sends every ACCEPT after the whole cycle.
 """
 from __future__ import annotations
 
@@ -401,7 +404,7 @@ class OfferProcessor:
     def __init__(self, client, persister, scheduler_config=None, token_bucket: Optional[TokenBucket] = None,
                  queue_capacity: int = DEFAULT_QUEUE_CAPACITY, offer_wait_s: Optional[float] = None,
                  hold_s: float = 0.0, event_driven: bool = False, gc_all_offers: bool = False,
-                 fast_unsuppress: bool = False, merge_agent_offers: bool = False):
+                 fast_unsuppress: bool = False, merge_agent_offers: bool = False, stream_launches: bool = False):
         self.client = client
         self.persister = persister
         self.offer_wait_s = offer_wait_s if offer_wait_s is not None else (
@@ -419,6 +422,8 @@ class OfferProcessor:
         # gc_all_offers collects them from every offer, idle or not.
         self.gc_all_offers = gc_all_offers
         self.merge_agent_offers = merge_agent_offers
+        # ACCEPT each step's launch as soon as it is matched instead of after the whole cycle
+        self.stream_launches = stream_launches
         self._held: Dict[str, tuple] = {}  # (real) offer id -> (offer, hold deadline)
         self._initialized = False
         self._deregistered = False
@@ -577,7 +582,24 @@ class OfferProcessor:
             if un.result == UnexpectedResult.PROCESSED and un.offer_resources:
                 pre_cleanup = to_cleanup_recommendations(un.offer_resources)
                 eval_offers = recycled_offers(offers, un.offer_resources)
-        resp = self.client.offers(eval_offers)
+        streamed_pre = set()
+        stream = None
+        if self.stream_launches:
+            pre_by_offer: Dict[str, list] = {}
+            for r in pre_cleanup:
+                pre_by_offer.setdefault(r.offer_id.value, []).append(r)
+
+            def stream(recs):
+                # the agent's stale-reservation cleanup goes at the head of the same ACCEPT
+                head = []
+                for oid in {r.offer_id.value for r in recs}:
+                    for r in pre_by_offer.pop(oid, ()):
+                        streamed_pre.add(id(r))
+                        head.append(r)
+                metrics.increment_recommendations(head + list(recs))
+                self.accepter.accept(head + list(recs), members)
+        resp = self.client.offers(eval_offers, launch_stream=stream) if stream is not None else \
+            self.client.offers(eval_offers)
         cleanup_recs = []
         unused = filter_out_accepted(offers, list(resp.recommendations) + pre_cleanup)
         if not self.gc_all_offers and unused:
@@ -608,7 +630,10 @@ class OfferProcessor:
                 for o in unused:
                     self._held.pop(o.id.value, None)
                 decline_short(unused)
-        all_recs = pre_cleanup + list(resp.recommendations) + cleanup_recs
+        if resp.streamed:
+            all_recs = [r for r in pre_cleanup if id(r) not in streamed_pre] + cleanup_recs
+        else:
+            all_recs = pre_cleanup + list(resp.recommendations) + cleanup_recs
         metrics.increment_recommendations(all_recs)
         self.accepter.accept(all_recs, members)
 

@@ -93,11 +93,13 @@ class AbstractScheduler(MesosEventClient):
         self.launch_watchdog.poll()
         return self.get_status()
 
-    def offers(self, offers) -> OfferResponse:
+    def offers(self, offers, launch_stream=None) -> OfferResponse:
         self.reconciler.reconcile()
         if not self.reconciler.is_reconciled():
             self.logger.info("Not ready for offers: waiting for task reconciliation to complete.")
             return OfferResponse.not_ready([])
+        if launch_stream is not None and self.supports_launch_stream:
+            return self.process_offers(offers, self.candidate_steps, launch_stream)
         return self.process_offers(offers, self.candidate_steps)
 
     def task_status(self, status) -> TaskStatusResponse:
@@ -131,6 +133,9 @@ class AbstractScheduler(MesosEventClient):
 
     def get_status(self):
         raise NotImplementedError
+
+    # process_offers(offers, steps, launch_stream) is implemented (see DefaultScheduler)
+    supports_launch_stream = False
 
     def process_offers(self, offers, steps) -> OfferResponse:
         raise NotImplementedError

@@ -174,23 +174,40 @@ class DefaultScheduler(AbstractScheduler):
             return ClientStatusResponse.launching(self.work_set_tracker.has_new_work())
         return ClientStatusResponse.idle()
 
-    def process_offers(self, offers, steps) -> OfferResponse:
-        recs = self.plan_scheduler.resource_offers(offers, steps)
+    supports_launch_stream = True
+
+    def _record(self, recs) -> bool:
+        """Write-ahead: persist the launches before anything is sent to the master."""
         try:
             self.launch_recorder.record(recs)
             if self.decommission_recorder is not None:
                 self.decommission_recorder.record_decommission(recs)
-            if self.launch_watchdog.enabled:
-                for r in recs:
-                    if isinstance(r, LaunchOfferRecommendation):
-                        st = P.TaskStatus(state=P.TASK_STAGING)
-                        st.task_id.CopyFrom(r.task_info.task_id)
-                        st.agent_id.CopyFrom(r.task_info.agent_id)
-                        self.launch_watchdog.launched(st)
         except Exception:  # noqa: BLE001
-            self.logger.exception("Failed to record offer operations, returning empty operations list")
-            recs = []
-        return OfferResponse.processed(recs)
+            self.logger.exception("Failed to record offer operations, dropping them")
+            return False
+        if self.launch_watchdog.enabled:
+            for r in recs:
+                if isinstance(r, LaunchOfferRecommendation):
+                    st = P.TaskStatus(state=P.TASK_STAGING)
+                    st.task_id.CopyFrom(r.task_info.task_id)
+                    st.agent_id.CopyFrom(r.task_info.agent_id)
+                    self.launch_watchdog.launched(st)
+        return True
+
+    def process_offers(self, offers, steps, launch_stream=None) -> OfferResponse:
+        if launch_stream is None:
+            recs = self.plan_scheduler.resource_offers(offers, steps)
+            return OfferResponse.processed(recs if self._record(recs) else [])
+
+        # Launch streaming: each step's launch is recorded and sent to the master as soon as the
+        # step is matched, so pods launch (and their agents start them) while later steps are
+        # still being evaluated, instead of after the whole cycle.
+        def on_step(recs):
+            if not self._record(recs):
+                return []
+            launch_stream(recs)
+            return recs
+        return OfferResponse.processed(self.plan_scheduler.resource_offers(offers, steps, on_step), streamed=True)
 
     def get_unexpected_resources(self, unused_offers) -> UnexpectedResourcesResponse:
         try:

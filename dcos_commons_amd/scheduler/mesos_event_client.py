@@ -80,19 +80,23 @@ class OfferResult(enum.Enum):
 
 
 class OfferResponse:
-    __slots__ = ("result", "recommendations")
+    """``streamed``: the recommendations were already sent to the master through the
+    ``launch_stream`` callback; the caller must not ACCEPT them again."""
 
-    def __init__(self, result: OfferResult, recommendations):
+    __slots__ = ("result", "recommendations", "streamed")
+
+    def __init__(self, result: OfferResult, recommendations, streamed: bool = False):
         self.result = result
         self.recommendations = list(recommendations)
+        self.streamed = streamed
 
     @staticmethod
     def not_ready(recs=()) -> "OfferResponse":
         return OfferResponse(OfferResult.NOT_READY, recs)
 
     @staticmethod
-    def processed(recs) -> "OfferResponse":
-        return OfferResponse(OfferResult.PROCESSED, recs)
+    def processed(recs, streamed: bool = False) -> "OfferResponse":
+        return OfferResponse(OfferResult.PROCESSED, recs, streamed)
 
 
 class UnexpectedResult(enum.Enum):
@@ -162,7 +166,10 @@ class MesosEventClient:
     def get_client_status(self) -> ClientStatusResponse:
         raise NotImplementedError
 
-    def offers(self, offers) -> OfferResponse:
+    def offers(self, offers, launch_stream=None) -> OfferResponse:
+        """``launch_stream(recs)``, when the client supports it, sends one step's recorded
+        recommendations to the master before the next step is evaluated; those recommendations
+        are then returned with ``OfferResponse.streamed`` set on them."""
         raise NotImplementedError
 
     def get_unexpected_resources(self, unused_offers) -> UnexpectedResourcesResponse:

@@ -358,7 +358,7 @@ class MultiServiceEventClient(MesosEventClient):
                 self.uninstall_callback(s.service_spec.name)
         return resp
 
-    def offers(self, offers) -> OfferResponse:
+    def offers(self, offers, launch_stream=None) -> OfferResponse:
         if not self.services_to_offer:
             return OfferResponse.processed([])
         recs, remaining, not_ready = [], list(offers), False

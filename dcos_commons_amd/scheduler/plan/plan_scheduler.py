@@ -23,7 +23,9 @@ class PlanScheduler:
         self.state_store = state_store
         self.logger = get_logger(__name__, namespace)
 
-    def resource_offers(self, offers, steps) -> list:
+    def resource_offers(self, offers, steps, on_step=None) -> list:
+        """``on_step(recs)``, when given, receives each step's recommendations as soon as that
+        step is matched (launch streaming); its return value replaces them in the result."""
         all_recs = []
         available = list(offers)
         # Launches are only recorded after the whole cycle (write-ahead, then ACCEPT), so the
@@ -32,8 +34,10 @@ class PlanScheduler:
         for step in steps:
             recs = self._step_offers(available, step, all_tasks)
             if recs:
-                all_recs.extend(recs)
                 used = {r.offer_id.value for r in recs}
+                if on_step is not None:
+                    recs = on_step(recs)
+                all_recs.extend(recs)
                 available = [o for o in available if o.id.value not in used]
         return all_recs
 

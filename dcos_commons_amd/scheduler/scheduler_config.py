@@ -261,6 +261,11 @@ class SchedulerConfig:
         """First REVIVE after a SUPPRESS skips the burst spacing (reference: never)."""
         return self.env.get_optional_boolean("SDK_FAST_UNSUPPRESS", True)
 
+    def is_stream_launches(self) -> bool:
+        """ACCEPT each matched step's launch immediately instead of after the whole offer cycle
+        (reference: one batch of ACCEPTs at the end of the cycle)."""
+        return self.env.get_optional_boolean("SDK_STREAM_LAUNCHES", True)
+
     def launch_reconcile_s(self) -> float:
         """Explicitly reconcile a launch that still has no status after this many seconds, e.g.
         because its ACCEPT was lost (0 = reference behaviour: wait for the next scheduler

@@ -294,7 +294,7 @@ class UninstallScheduler:
             return ClientStatusResponse.ready_to_remove()
         return ClientStatusResponse.launching(self.work_set_tracker.has_new_work())
 
-    def offers(self, offers) -> OfferResponse:
+    def offers(self, offers, launch_stream=None) -> OfferResponse:
         self.reconciler.reconcile()
         if not self.reconciler.is_reconciled():
             return OfferResponse.not_ready([])
