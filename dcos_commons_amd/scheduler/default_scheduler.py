@@ -241,7 +241,9 @@ class DefaultScheduler(AbstractScheduler):
     def process_status_update(self, status: P.TaskStatus) -> None:
         info = state_store_utils.fetch_task_info(self.state_store, status)
         name = info.name
-        if self.unknown_as_lost and _never_launched(self.state_store.fetch_status(name), status):
+        if (self.unknown_as_lost and status.state in _NEVER_LAUNCHED_STATES
+                and status.reason in _NEVER_LAUNCHED_REASONS
+                and _never_launched(self.state_store.fetch_status(name), status)):
             # The launch was recorded (write-ahead) but its ACCEPT never took effect, so the
             # reservations in the stored TaskInfo do not exist and an in-place relaunch would
             # wait for them forever. Mark it permanently failed: the step relaunches with a fresh
