@@ -1,0 +1,427 @@
+"""Framework layer: OfferQueue, OfferProcessor cycles, TaskKiller, ImplicitReconciler,
+FrameworkScheduler callbacks.
+
+Pinned against the reference's framework suite
+(sdk/scheduler/src/test/java/com/mesosphere/sdk/framework/OfferQueueTest.java, OfferProcessorTest
+.java incl. the 50-thread enqueue test, TaskKillerTest.java, ImplicitReconcilerTest.java,
+FrameworkSchedulerTest.java): a recording driver stands in for the mocked SchedulerDriver.
+"""
+import threading
+import time
+import uuid
+
+import pytest
+
+from dcos_commons_amd.framework import driver, task_killer
+from dcos_commons_amd.framework.offer_processing import (
+    ImplicitReconciler,
+    OfferProcessor,
+    OfferQueue,
+)
+from dcos_commons_amd.mesos import protos as P
+from dcos_commons_amd.offer.recommendations import (
+    ReserveOfferRecommendation,
+)
+from dcos_commons_amd.scheduler.mesos_event_client import (
+    ClientStatusResponse,
+    OfferResources,
+    OfferResponse,
+    UnexpectedResourcesResponse,
+)
+from dcos_commons_amd.storage.mem_persister import MemPersister
+
+
+class RecordingDriver:
+    def __init__(self):
+        self.lock = threading.Lock()
+        self.accepts, self.declines, self.kills, self.reconciles = [], [], [], []
+        self.revives = self.suppresses = 0
+
+    def accept_offers(self, offer_ids, operations, filters=None):
+        with self.lock:
+            self.accepts.append(([o.value for o in offer_ids], [op.type for op in operations]))
+
+    def decline_offer(self, offer_id, filters=None):
+        self.decline_offers([offer_id], filters)
+
+    def decline_offers(self, offer_ids, filters=None):
+        with self.lock:
+            self.declines.append(([o.value for o in offer_ids], filters.refuse_seconds if filters else None))
+
+    def kill_task(self, task_id):
+        with self.lock:
+            self.kills.append(task_id.value)
+
+    def reconcile_tasks(self, statuses):
+        with self.lock:
+            self.reconciles.append([s.task_id.value for s in statuses])
+
+    def revive_offers(self):
+        self.revives += 1
+
+    def suppress_offers(self):
+        self.suppresses += 1
+
+    def declined_ids(self):
+        return {i for ids, _ in self.declines for i in ids}
+
+
+@pytest.fixture
+def drv():
+    d = RecordingDriver()
+    driver.set_driver(d)
+    task_killer.reset(executor_enabled=False)
+    yield d
+    task_killer.reset(executor_enabled=False)
+    driver.set_driver(None)
+
+
+def offer(oid=None, cpus=1.0, agent="agent-1", reserved_id=None):
+    o = P.Offer(hostname="host")
+    o.id.value = oid or str(uuid.uuid4())
+    o.agent_id.value, o.framework_id.value = agent, "fw"
+    r = o.resources.add(name="cpus", type=P.Value.SCALAR)
+    r.scalar.value = cpus
+    if reserved_id:
+        res = r.reservations.add(type=P.Resource.ReservationInfo.DYNAMIC, role="svc-role", principal="p")
+        res.labels.labels.add(key="resource_id", value=reserved_id)
+    return o
+
+
+class Client:
+    """A scripted MesosEventClient."""
+
+    def __init__(self, status=None, offers_fn=None, unexpected_fn=None):
+        self.status = status or ClientStatusResponse.launching(False)
+        self.offers_fn = offers_fn or (lambda offers: OfferResponse.processed([]))
+        self.unexpected_fn = unexpected_fn or (lambda offers: UnexpectedResourcesResponse.processed([]))
+        self.received = []
+        self.lock = threading.Lock()
+
+    def get_client_status(self):
+        return self.status
+
+    def offers(self, offers, launch_stream=None):
+        with self.lock:
+            self.received.extend(o.id.value for o in offers)
+        return self.offers_fn(offers)
+
+    def get_unexpected_resources(self, offers):
+        return self.unexpected_fn(offers)
+
+    def unregistered(self):
+        pass
+
+
+def processor(client, **kw):
+    p = OfferProcessor(client, MemPersister(), **kw)
+    return p
+
+
+# ---------------------------------------------------------------------------------------
+# OfferQueue
+
+
+def test_offer_queue_basics():
+    q = OfferQueue(capacity=3)
+    assert q.is_empty() and q.take_all(0) == []
+    os_ = [offer(f"o{i}") for i in range(4)]
+    assert [q.offer(o) for o in os_] == [True, True, True, False]   # capacity
+    assert q.size() == 3
+    assert not q.remove(P.OfferID(value="unknown"))
+    assert q.remove(P.OfferID(value="o1"))
+    assert [o.id.value for o in q.take_all(0)] == ["o0", "o2"]
+    assert q.is_empty()
+    assert not q.remove(P.OfferID(value="o0"))          # remove from an empty queue
+
+
+def test_offer_queue_take_waits_and_wakes():
+    q = OfferQueue()
+    t0 = time.monotonic()
+    assert q.take_all(0.05) == []
+    assert time.monotonic() - t0 >= 0.045
+    threading.Timer(0.02, lambda: q.offer(offer("late"))).start()
+    got = q.take_all(2.0)
+    assert [o.id.value for o in got] == ["late"]
+    wake = threading.Event()
+    threading.Timer(0.02, wake.set).start()
+    t0 = time.monotonic()
+    assert q.take_all(2.0, wake) == [] and time.monotonic() - t0 < 1.0
+
+
+# ---------------------------------------------------------------------------------------
+# OfferProcessor cycles (synchronous)
+
+
+def test_unused_offers_declined_long_when_idle(drv):
+    p = processor(Client(status=ClientStatusResponse.idle())).disable_threading()
+    p.start()
+    p.enqueue([offer("a"), offer("b")])
+    assert drv.declined_ids() == {"a", "b"}
+    assert all(refuse == 3600 for _, refuse in drv.declines)
+    assert drv.suppresses == 1
+
+
+def test_not_ready_offers_declined_short(drv):
+    c = Client(offers_fn=lambda offers: OfferResponse.not_ready([]))
+    p = processor(c).disable_threading()
+    p.start()
+    p.enqueue([offer("a")])
+    assert drv.declines == [(["a"], 5)]
+
+
+def test_unused_offers_declined_long_while_working_without_holding(drv):
+    p = processor(Client()).disable_threading()
+    p.start()
+    p.enqueue([offer("a")])
+    assert drv.declines == [(["a"], 3600)]
+
+
+def test_held_offers_are_reevaluated_then_declined(drv):
+    c = Client()
+    p = processor(c, hold_s=0.05).disable_threading()
+    p.start()
+    p.enqueue([offer("a")])
+    assert drv.declines == [] and c.received == ["a"]
+    p.process_queued_offers(0)                       # the held offer is evaluated again
+    assert c.received == ["a", "a"]
+    time.sleep(0.06)
+    p.process_queued_offers(0)
+    assert drv.declines == [(["a"], 5)]              # expired holds go back short
+
+
+def test_accepted_and_unexpected_resources(drv):
+    """Recommendations are accepted; unused offers' unexpected reservations are released in one
+    ACCEPT with DESTROY before UNRESERVE (OfferProcessor.java:300-330)."""
+    def offers_fn(offers):
+        o = offers[0]
+        return OfferResponse.processed([ReserveOfferRecommendation(o, o.resources[0])])
+
+    def unexpected_fn(offers):
+        out = []
+        for o in offers:
+            if o.id.value == "stale":
+                vol = P.Resource()
+                vol.CopyFrom(o.resources[0])
+                vol.disk.persistence.id = "pid"
+                out.append(OfferResources(o, [o.resources[0], vol]))
+        return UnexpectedResourcesResponse.processed(out)
+    p = processor(Client(offers_fn=offers_fn, unexpected_fn=unexpected_fn)).disable_threading()
+    p.start()
+    p.enqueue([offer("used", agent="agent-1"), offer("stale", agent="agent-2", reserved_id="old")])
+    by_offer = {ids[0]: ops for ids, ops in drv.accepts}
+    assert by_offer["used"] == [P.Offer.Operation.RESERVE]
+    ops = by_offer["stale"]
+    assert ops.index(P.Offer.Operation.DESTROY) < ops.index(P.Offer.Operation.UNRESERVE)
+    assert "stale" not in drv.declined_ids()
+
+
+def test_uninstalled_client_tears_down(drv):
+    torn = []
+
+    class D(RecordingDriver):
+        def teardown(self):
+            torn.append(True)
+
+        def stop(self, failover=True):
+            torn.append(failover)
+    d = D()
+    driver.set_driver(d)
+    from dcos_commons_amd.scheduler.mesos_event_client import IdleRequest
+
+    st = ClientStatusResponse.idle()
+    st.idle_request = IdleRequest.REMOVE_CLIENT
+    p = processor(Client(status=st)).disable_threading()
+    p.start()
+    p.enqueue([offer("a")])
+    assert torn == [True, False]
+
+
+@pytest.mark.parametrize("capacity,expect_declines", [(0, False), (10, True)])
+def test_fifty_threads_enqueue(drv, capacity, expect_declines):
+    """OfferProcessorTest.testAsyncOffers{Unlimited,Limited}QueueSize: 50 threads x 3 offers."""
+    c = Client(offers_fn=lambda offers: OfferResponse.processed(
+        [ReserveOfferRecommendation(o, o.resources[0]) for o in offers]))
+    p = processor(c, queue_capacity=capacity, offer_wait_s=0.01)
+    p.start()
+    sent = []
+    lock = threading.Lock()
+
+    def send():
+        os_ = [offer() for _ in range(3)]
+        with lock:
+            sent.extend(o.id.value for o in os_)
+        p.enqueue(os_)
+    ts = [threading.Thread(target=send) for _ in range(50)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    p.await_offers_processed(10)
+    p.stop()
+    declined = drv.declined_ids()
+    assert set(c.received) | declined == set(sent)
+    assert set(c.received) & declined == set()
+    if expect_declines:
+        assert declined                       # the bounded queue sheds load by declining
+    else:
+        assert not declined and len(c.received) == 150
+
+
+def test_stream_callback_accepts_before_the_cycle_ends(drv):
+    """Launch streaming: a client that streams gets its recs ACCEPTed from inside offers()."""
+    seen_during = []
+
+    class Streaming(Client):
+        def offers(self, offers, launch_stream=None):
+            o = offers[0]
+            recs = [ReserveOfferRecommendation(o, o.resources[0])]
+            launch_stream(recs)
+            seen_during.append(len(drv.accepts))
+            return OfferResponse.processed(recs, streamed=True)
+    p = processor(Streaming(), stream_launches=True).disable_threading()
+    p.start()
+    p.enqueue([offer("a")])
+    assert seen_during == [1]
+    assert drv.accepts == [(["a"], [P.Offer.Operation.RESERVE])]     # not accepted twice
+
+
+# ---------------------------------------------------------------------------------------
+# TaskKiller
+
+
+def test_task_killer_breaks_the_kill_loop(drv):
+    tid = P.TaskID(value="svc__pod-0-task__1")
+    task_killer.kill_task(tid)
+    assert drv.kills == [tid.value] and task_killer.pending_kills() == {tid.value}
+    lost = P.TaskStatus(state=P.TASK_LOST)
+    lost.task_id.CopyFrom(tid)
+    # the expected death completes the kill and is NOT eligible for another kill
+    assert task_killer.update(lost) is False
+    assert task_killer.pending_kills() == set()
+    # an unexpected death is eligible (it was not scheduled for killing)
+    assert task_killer.update(lost) is True
+    running = P.TaskStatus(state=P.TASK_RUNNING)
+    running.task_id.CopyFrom(tid)
+    assert task_killer.update(running) is True
+
+
+def test_task_killer_ignores_empty_ids_and_rekills(drv):
+    task_killer.kill_task(P.TaskID(value=""))
+    assert drv.kills == []
+    task_killer.kill_task(P.TaskID(value="a"))
+    task_killer.kill_task(P.TaskID(value="b"))
+    task_killer.kill_all_tasks()
+    assert sorted(drv.kills) == ["a", "a", "b", "b"]
+
+
+# ---------------------------------------------------------------------------------------
+# ImplicitReconciler
+
+
+def test_implicit_reconciler(drv):
+    r = ImplicitReconciler(0.0, 3600.0).disable_threading()
+    r.start()
+    assert drv.reconciles == [[]]           # single-threaded: reconciles once, immediately
+    with pytest.raises(RuntimeError):
+        r.start()
+    threaded = ImplicitReconciler(0.0, 0.02)
+    threaded.start()
+    time.sleep(0.15)
+    threaded.stop()
+    assert len(drv.reconciles) >= 3
+
+
+# ---------------------------------------------------------------------------------------
+# FrameworkScheduler callbacks
+
+
+class _StatusClient(Client):
+    def __init__(self, known=()):
+        super().__init__()
+        self.known = set(known)
+        self.statuses = []
+        self.registrations = []
+
+    def registered(self, re_registered):
+        self.registrations.append(re_registered)
+
+    def task_status(self, status):
+        from dcos_commons_amd.scheduler.mesos_event_client import TaskStatusResponse
+
+        self.statuses.append(status.task_id.value)
+        return TaskStatusResponse.processed() if status.task_id.value in self.known else \
+            TaskStatusResponse.unknown_task()
+
+
+def _fs(client, persister=None):
+    from dcos_commons_amd.framework.framework_scheduler import FrameworkScheduler
+    from dcos_commons_amd.state.framework_store import FrameworkStore
+
+    persister = persister or MemPersister()
+    fs = FrameworkScheduler({"svc-role"}, None, persister, FrameworkStore(persister), client)
+    return fs.disable_threading(), FrameworkStore(persister)
+
+
+def test_register_stores_framework_id_and_reregister(drv):
+    c = _StatusClient()
+    fs, store = _fs(c)
+    fs.registered(drv, P.FrameworkID(value="fw-1"), None)
+    assert store.fetch_framework_id().value == "fw-1"
+    fs.registered(drv, P.FrameworkID(value="fw-1"), None)     # a second registration is a re-registration
+    assert c.registrations == [False, True]
+
+
+def test_offers_declined_until_api_server_started(drv):
+    c = _StatusClient()
+    fs, _ = _fs(c)
+    fs.registered(drv, P.FrameworkID(value="fw-1"), None)
+    fs.resource_offers(drv, [offer("early")])
+    assert drv.declines == [(["early"], 5)] and c.received == []
+    fs.set_api_server_started()
+    fs.resource_offers(drv, [offer("later")])
+    assert c.received == ["later"]
+
+
+def test_offer_rescinded_is_dequeued(drv):
+    c = _StatusClient()
+    fs, _ = _fs(c)
+    fs.offer_processor.multithreaded = True          # keep offers queued (no synchronous processing)
+    fs.set_api_server_started()
+    fs.offer_processor.enqueue([offer("x"), offer("y")])
+    fs.offer_rescinded(drv, P.OfferID(value="x"))
+    assert [o.id.value for o in fs.offer_processor.queue.take_all(0)] == ["y"]
+
+
+def test_foreign_reservations_are_filtered(drv):
+    c = _StatusClient()
+    fs, _ = _fs(c)
+    fs.registered(drv, P.FrameworkID(value="fw-1"), None)
+    fs.set_api_server_started()
+    got = []
+    fs.offer_processor.enqueue = lambda offers: got.extend(offers)
+    o = offer("o")
+    foreign = o.resources.add(name="mem", type=P.Value.SCALAR)
+    foreign.scalar.value = 64
+    res = foreign.reservations.add(type=P.Resource.ReservationInfo.DYNAMIC, role="other-role", principal="x")
+    res.labels.labels.add(key="resource_id", value="theirs")
+    fs.resource_offers(drv, [o])
+    assert [r.name for r in got[0].resources] == ["cpus"]
+
+
+def test_unknown_task_status_kills_once(drv):
+    c = _StatusClient(known={"known"})
+    fs, _ = _fs(c)
+    st = P.TaskStatus(state=P.TASK_RUNNING)
+    st.task_id.value = "stray"
+    fs.status_update(drv, st)
+    assert drv.kills == ["stray"]
+    # the master answers the kill of an unknown task with LOST: no kill loop
+    lost = P.TaskStatus(state=P.TASK_LOST, reason=P.TaskStatus.REASON_RECONCILIATION)
+    lost.task_id.value = "stray"
+    fs.status_update(drv, lost)
+    assert drv.kills == ["stray"]
+    ok = P.TaskStatus(state=P.TASK_RUNNING)
+    ok.task_id.value = "known"
+    fs.status_update(drv, ok)
+    assert drv.kills == ["stray"] and c.statuses == ["stray", "stray", "known"]
