@@ -240,8 +240,14 @@ def test_uninstalled_client_tears_down(drv):
 @pytest.mark.parametrize("capacity,expect_declines", [(0, False), (10, True)])
 def test_fifty_threads_enqueue(drv, capacity, expect_declines):
     """OfferProcessorTest.testAsyncOffers{Unlimited,Limited}QueueSize: 50 threads x 3 offers."""
-    c = Client(offers_fn=lambda offers: OfferResponse.processed(
-        [ReserveOfferRecommendation(o, o.resources[0]) for o in offers]))
+    gate = threading.Event()
+    if not expect_declines:
+        gate.set()
+
+    def offers_fn(offers):
+        gate.wait(10)            # bounded case: the processor stalls while the threads pile offers up
+        return OfferResponse.processed([ReserveOfferRecommendation(o, o.resources[0]) for o in offers])
+    c = Client(offers_fn=offers_fn)
     p = processor(c, queue_capacity=capacity, offer_wait_s=0.01)
     p.start()
     sent = []
@@ -257,6 +263,7 @@ def test_fifty_threads_enqueue(drv, capacity, expect_declines):
         t.start()
     for t in ts:
         t.join()
+    gate.set()
     p.await_offers_processed(10)
     p.stop()
     declined = drv.declined_ids()
