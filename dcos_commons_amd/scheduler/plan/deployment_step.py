@@ -96,8 +96,10 @@ class DeploymentStep(AbstractStep):
         return display_status(self.state_store, AbstractStep.get_status(self), names)
 
     def update(self, status: P.TaskStatus) -> None:
+        tid = status.task_id.value
+        if tid not in self._tasks:      # every step of every plan sees every status: skip lock-free
+            return
         with self._status_lock:
-            tid = status.task_id.value
             if tid not in self._tasks:
                 return
             if self.is_complete():

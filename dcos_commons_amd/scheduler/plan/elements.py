@@ -278,6 +278,11 @@ class AbstractStep(Step):
         return self._name
 
     def get_status(self) -> Status:
+        # Hot path (strategies and aggregate statuses read every step, every cycle): a plain
+        # attribute read is atomic, so only the states with side conditions take the lock.
+        st = self._status
+        if st is not Status.DELAYED and not self._interrupted:
+            return st
         with self._status_lock:
             if self._interrupted and self._status in (Status.PENDING, Status.PREPARED):
                 return Status.WAITING

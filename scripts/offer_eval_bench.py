@@ -69,6 +69,7 @@ def main():
     ap.add_argument("--pods", type=int, default=8)
     ap.add_argument("--reps", type=int, default=30)
     ap.add_argument("--profile", action="store_true")
+    ap.add_argument("--sort", default="tottime", help="cProfile sort key (tottime, cumulative)")
     a = ap.parse_args()
     one_pass(a.pods)
     prof = cProfile.Profile() if a.profile else None
@@ -80,7 +81,7 @@ def main():
     print(f"pods={a.pods} median pass {med:.2f} ms, {med / a.pods:.3f} ms/pod (min {ts[0] * 1000:.2f})")
     if prof:
         out = io.StringIO()
-        pstats.Stats(prof, stream=out).sort_stats("tottime").print_stats(40)
+        pstats.Stats(prof, stream=out).sort_stats(a.sort).print_stats(40)
         print(out.getvalue())
 
 
