@@ -148,9 +148,11 @@ class PodInfoBuilder:
         w = L.TaskLabelWriter(t).set_target_configuration(target_config_id).set_type(pod.type).set_index(pi.index)
         w.set_additional_labels(ts.labels)
         w.apply()
+        # the command, health check and readiness check all start from the same task environment
+        base_env = L.env_from_map(get_task_environment(service_name, pi, ts, scheduler_config))
         if ts.command is not None:
             cmd = t.command
-            cmd.environment.CopyFrom(L.env_from_map(get_task_environment(service_name, pi, ts, scheduler_config)))
+            cmd.environment.CopyFrom(base_env)
             if override == GoalStateOverride.PAUSED:
                 cmd.value = scheduler_config.pause_override_cmd()
             else:
@@ -185,8 +187,8 @@ class PodInfoBuilder:
             t.container.linux_info.ipc_mode = P.LinuxInfo.IpcMode.Value(ts.shared_memory.value)
         if ts.shared_memory_size is not None:
             t.container.linux_info.shm_size = ts.shared_memory_size
-        self._set_health_check(t, service_name, pi, ts, override, scheduler_config)
-        self._set_readiness_check(t, service_name, pi, ts, override, scheduler_config)
+        self._set_health_check(t, service_name, pi, ts, override, scheduler_config, base_env)
+        self._set_readiness_check(t, service_name, pi, ts, override, scheduler_config, base_env)
         if ts.kill_grace_period < 0:
             raise InvalidRequirementException(
                 f"kill-grace-period must be zero or a positive integer, received: {ts.kill_grace_period}")
@@ -194,7 +196,7 @@ class PodInfoBuilder:
         return t
 
     @staticmethod
-    def _set_health_check(t, service_name, pi, ts, override, scheduler_config) -> None:
+    def _set_health_check(t, service_name, pi, ts, override, scheduler_config, env=None) -> None:
         hc = ts.health_check
         if hc is None or override == GoalStateOverride.PAUSED:
             return
@@ -206,10 +208,11 @@ class PodInfoBuilder:
         h.grace_period_seconds = hc.grace_period
         h.type = P.HealthCheck.COMMAND
         h.command.value = hc.command
-        h.command.environment.CopyFrom(L.env_from_map(get_task_environment(service_name, pi, ts, scheduler_config)))
+        h.command.environment.CopyFrom(
+            env if env is not None else L.env_from_map(get_task_environment(service_name, pi, ts, scheduler_config)))
 
     @staticmethod
-    def _set_readiness_check(t, service_name, pi, ts, override, scheduler_config) -> None:
+    def _set_readiness_check(t, service_name, pi, ts, override, scheduler_config, env=None) -> None:
         rc = ts.readiness_check
         if override == GoalStateOverride.PAUSED:
             rc = ReadinessCheckSpec(PAUSE_READINESS_COMMAND, constants.SHORT_DECLINE_SECONDS,
@@ -223,7 +226,7 @@ class PodInfoBuilder:
         c.timeout_seconds = rc.timeout
         c.command.command.value = rc.command
         c.command.command.environment.CopyFrom(
-            L.env_from_map(get_task_environment(service_name, pi, ts, scheduler_config)))
+            env if env is not None else L.env_from_map(get_task_environment(service_name, pi, ts, scheduler_config)))
 
     @staticmethod
     def _executor_info(pi: PodInstance, framework_id: P.FrameworkID, scheduler_config) -> P.ExecutorInfo:

@@ -59,11 +59,15 @@ class OfferEvaluationStage:
 
 
 class ReserveEvaluationOutcome:
-    __slots__ = ("outcome", "resource_id")
+    """``resource``: for a brand-new reservation of exactly the spec's value, the reserved
+    resource as built from the spec (the task carries the same resource, so it is not rebuilt)."""
 
-    def __init__(self, outcome: EvaluationOutcome, resource_id: Optional[str]):
+    __slots__ = ("outcome", "resource_id", "resource")
+
+    def __init__(self, outcome: EvaluationOutcome, resource_id: Optional[str], resource=None):
         self.outcome = outcome
         self.resource_id = resource_id
+        self.resource = resource
 
 
 def evaluate_simple_resource(stage, spec: ResourceSpec, resource_id: Optional[str], namespace: Optional[str],
@@ -85,10 +89,14 @@ def evaluate_simple_resource(stage, spec: ResourceSpec, resource_id: Optional[st
             resource = ResourceBuilder.from_spec(spec, None, namespace, framework_id).set_mesos_resource(mr).build()
             rec = ReserveOfferRecommendation(pool.offer, resource)
             new_id = get_resource_id(resource)
+            # an offered chunk that carried nothing beyond name/type/value/(pre-)reservations builds
+            # to exactly what ResourceBuilder.from_spec(spec, new_id) would produce for the task
+            plain = not (mr.resource.HasField("disk") or mr.resource.HasField("provider_id")
+                         or len(mr.resource.reservations) or mr.resource.HasField("reservation"))
             return ReserveEvaluationOutcome(EvaluationOutcome.pass_(
                 stage, "Offer contains sufficient unreserved '%s', generated new resourceId: '%s' "
                        "for new reservation: '%s'", spec.name, new_id, spec,
-                recommendations=[rec], mesos_resource=mr), new_id)
+                recommendations=[rec], mesos_resource=mr), new_id, resource if plain else None)
         return ReserveEvaluationOutcome(EvaluationOutcome.pass_(
             stage, "Offer contains previously reserved '%s' with resourceId: '%s' for resource: '%s'",
             spec.name, resource_id, spec, mesos_resource=mr), resource_id)
@@ -188,7 +196,8 @@ class ResourceEvaluationStage(OfferEvaluationStage):
         res = evaluate_simple_resource(self, self.spec, self.resource_id, self.namespace, pool, self.framework_id)
         if not res.outcome.passing:
             return res.outcome
-        resource = ResourceBuilder.from_spec(self.spec, res.resource_id, self.namespace, self.framework_id).build()
+        resource = res.resource if res.resource is not None else \
+            ResourceBuilder.from_spec(self.spec, res.resource_id, self.namespace, self.framework_id).build()
         for t in self.task_names:
             set_protos(builder, resource, t)
         if not self.task_names:
