@@ -49,8 +49,8 @@ def _never_launched(prev: Optional[P.TaskStatus], status: P.TaskStatus) -> bool:
             and status.reason in _NEVER_LAUNCHED_REASONS)
 
 
-def _is_working(plan) -> bool:
-    st = plan.get_status()
+def _is_working(plan, st: Optional[Status] = None) -> bool:
+    st = plan.get_status() if st is None else st
     if st in (Status.PENDING, Status.IN_PROGRESS, Status.PREPARED, Status.STARTED, Status.STARTING):
         return True
     if st in (Status.DELAYED, Status.COMPLETE, Status.ERROR, Status.WAITING):
@@ -158,8 +158,13 @@ class DefaultScheduler(AbstractScheduler):
 
     def get_status(self) -> ClientStatusResponse:
         pms = self.plan_coordinator.get_plan_managers()
-        all_delayed_or_complete = all(pm.get_plan().is_complete() or pm.get_plan().is_delayed() for pm in pms)
-        deploy_completed = self.deployment_plan_manager.get_plan().is_complete()
+        # each plan's status is an aggregate over all its steps: compute it once per call
+        statuses = [pm.get_plan().get_status() for pm in pms]
+        all_delayed_or_complete = all(st in (Status.COMPLETE, Status.DELAYED) for st in statuses)
+        deploy_st = next((st for pm, st in zip(pms, statuses) if pm is self.deployment_plan_manager), None)
+        if deploy_st is None:
+            deploy_st = self.deployment_plan_manager.get_plan().get_status()
+        deploy_completed = deploy_st == Status.COMPLETE
         if deploy_completed and not self._deployment_completion_stored:
             state_store_utils.set_deployment_was_completed(self.state_store)
             self._deployment_completion_stored = True
@@ -170,7 +175,7 @@ class DefaultScheduler(AbstractScheduler):
             return ClientStatusResponse.idle()
         if not deploy_completed or _is_replacing(self.recovery_plan_manager):
             return ClientStatusResponse.footprint(self.work_set_tracker.has_new_work())
-        if any(_is_working(pm.get_plan()) for pm in pms):
+        if any(_is_working(pm.get_plan(), st) for pm, st in zip(pms, statuses)):
             return ClientStatusResponse.launching(self.work_set_tracker.has_new_work())
         return ClientStatusResponse.idle()
 

@@ -29,7 +29,8 @@ def asset_conflicts(asset: PodInstanceRequirement, dirty_assets: Iterable[PodIns
 
 
 def is_eligible(element: "Element", dirty_assets) -> bool:
-    if element.is_complete() or element.has_errors():
+    # one status read: a parent's status is a full aggregate over its children
+    if element.get_status() in (Status.COMPLETE, Status.ERROR):
         return False
     if element.is_interrupted():
         return False
