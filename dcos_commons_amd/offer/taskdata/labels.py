@@ -36,6 +36,11 @@ VIP_OVERLAY_FLAG_VALUE = "container"
 VIP_BRIDGE_FLAG_VALUE = "host"
 # MI355X placement: which GPUs of the agent the task was given (comma-separated indices).
 GPU_DEVICES_LABEL = "gpu_devices"
+# This SDK only: set on the stored TaskInfo when every reservation it references was created by
+# the launch that wrote it (first launch or permanent replace), never on an in-place relaunch that
+# reuses existing reservations/volumes. Only such a launch may be re-footprinted when the master
+# reports it never saw the ACCEPT (see DefaultScheduler.process_status_update).
+LAUNCH_NEW_FOOTPRINT_LABEL = "launch_new_footprint"
 
 # EnvConstants
 POD_INSTANCE_INDEX_TASKENV = "POD_INSTANCE_INDEX"
@@ -204,6 +209,9 @@ class TaskLabelReader:
     def has_readiness_check_label(self) -> bool:
         return READINESS_CHECK_LABEL in self._labels
 
+    def is_launch_new_footprint(self) -> bool:
+        return self._labels.get(LAUNCH_NEW_FOOTPRINT_LABEL) == BOOLEAN_LABEL_TRUE_VALUE
+
     def get_readiness_check(self) -> Optional[P.HealthCheck]:
         v = self._labels.get(READINESS_CHECK_LABEL)
         return decode_health_check(v) if v else None
@@ -226,6 +234,13 @@ class TaskLabelWriter:
 
     def clear_permanently_failed(self):
         self._labels.pop(PERMANENTLY_FAILED_LABEL, None)
+        return self
+
+    def set_launch_new_footprint(self, new: bool):
+        if new:
+            self._labels[LAUNCH_NEW_FOOTPRINT_LABEL] = BOOLEAN_LABEL_TRUE_VALUE
+        else:
+            self._labels.pop(LAUNCH_NEW_FOOTPRINT_LABEL, None)
         return self
 
     def set_type(self, t: str):

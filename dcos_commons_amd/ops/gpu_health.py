@@ -45,15 +45,17 @@ def readiness_probe(device: int = 0) -> dict:
 
     t0 = time.perf_counter()
     dev = torch.device("cuda", device)
-    g = torch.Generator(device=dev)
-    g.manual_seed(4321 + device)
-    a = torch.randn((256, 512), generator=g, device=dev, dtype=torch.float32).to(torch.bfloat16)
-    bt = torch.randn((256, 512), generator=g, device=dev, dtype=torch.float32).to(torch.bfloat16)
-    c = ops.gemm_bf16_nt(a, bt)
-    rel = freivalds_rel_err(a, bt, c, g)
-    buf = torch.empty(16 * 2**20, dtype=torch.int32, device=dev)  # 64 MiB
-    ops.pattern_write(buf, seed=device + 11)
-    bad = ops.pattern_check(buf, seed=device + 11)
+    # the HIP kernels launch on the current device's stream: make `device` current for the probe
+    with torch.cuda.device(dev):
+        g = torch.Generator(device=dev)
+        g.manual_seed(4321 + device)
+        a = torch.randn((256, 512), generator=g, device=dev, dtype=torch.float32).to(torch.bfloat16)
+        bt = torch.randn((256, 512), generator=g, device=dev, dtype=torch.float32).to(torch.bfloat16)
+        c = ops.gemm_bf16_nt(a, bt)
+        rel = freivalds_rel_err(a, bt, c, g)
+        buf = torch.empty(16 * 2**20, dtype=torch.int32, device=dev)  # 64 MiB
+        ops.pattern_write(buf, seed=device + 11)
+        bad = ops.pattern_check(buf, seed=device + 11)
     return {"device": device, "gemm_rel_err": rel, "mem_bad_words": bad,
             "healthy": bool(rel < MAX_GEMM_REL_ERR and bad == 0), "probe_seconds": round(time.perf_counter() - t0, 4)}
 

@@ -17,6 +17,7 @@ from dcos_commons_amd.offer.evaluate.offer_evaluator import OfferEvaluator
 from dcos_commons_amd.offer.history import OfferOutcomeTracker, OfferOutcomeTrackerV2
 from dcos_commons_amd.offer.recommendations import LaunchOfferRecommendation
 from dcos_commons_amd.offer.resources import get_all_resources, get_resource_id, get_resource_ids
+from dcos_commons_amd.offer.taskdata.labels import TaskLabelReader
 from dcos_commons_amd.scheduler.abstract_scheduler import AbstractScheduler
 from dcos_commons_amd.scheduler.decommission import DECOMMISSIONING_STATUS
 from dcos_commons_amd.scheduler.mesos_event_client import (
@@ -41,12 +42,18 @@ _NEVER_LAUNCHED_STATES = (P.TASK_LOST, P.TASK_DROPPED)
 _NEVER_LAUNCHED_REASONS = (P.TaskStatus.REASON_RECONCILIATION, P.TaskStatus.REASON_INVALID_OFFERS)
 
 
-def _never_launched(prev: Optional[P.TaskStatus], status: P.TaskStatus) -> bool:
+def _never_launched(info: P.TaskInfo, prev: Optional[P.TaskStatus], status: P.TaskStatus) -> bool:
     """The master reports a task it never saw (dropped ACCEPT, offer gone before the ACCEPT, or
-    forgotten) while our only record of it is the write-ahead STAGING status."""
+    forgotten) while our only record of it is the write-ahead STAGING status, AND that launch was
+    the one meant to create every reservation the task references (``launch_new_footprint``).
+
+    An in-place relaunch (transient recovery, pod restart, config rollout) reuses reservations and
+    persistent volumes that exist whether or not its ACCEPT arrived: it never qualifies, so it stays
+    a transient LOST and its volumes are kept."""
     return (prev is not None and prev.state == P.TASK_STAGING and prev.task_id.value == status.task_id.value
+            and info.task_id.value == status.task_id.value
             and status.source == P.TaskStatus.SOURCE_MASTER and status.state in _NEVER_LAUNCHED_STATES
-            and status.reason in _NEVER_LAUNCHED_REASONS)
+            and status.reason in _NEVER_LAUNCHED_REASONS and TaskLabelReader(info).is_launch_new_footprint())
 
 
 def _is_working(plan, st: Optional[Status] = None) -> bool:
@@ -248,11 +255,11 @@ class DefaultScheduler(AbstractScheduler):
         name = info.name
         if (self.unknown_as_lost and status.state in _NEVER_LAUNCHED_STATES
                 and status.reason in _NEVER_LAUNCHED_REASONS
-                and _never_launched(self.state_store.fetch_status(name), status)):
-            # The launch was recorded (write-ahead) but its ACCEPT never took effect, so the
-            # reservations in the stored TaskInfo do not exist and an in-place relaunch would
-            # wait for them forever. Mark it permanently failed: the step relaunches with a fresh
-            # footprint and anything that was reserved is garbage-collected as unexpected.
+                and _never_launched(info, self.state_store.fetch_status(name), status)):
+            # A first-footprint launch was recorded (write-ahead) but its ACCEPT never took
+            # effect, so the reservations in the stored TaskInfo were never made and an in-place
+            # relaunch would wait for them forever. Mark it permanently failed: the step relaunches
+            # with a fresh footprint and anything that was reserved is garbage-collected.
             self.logger.warning("Launch of %s never reached the master (%s, %s): relaunching with new reservations",
                                 name, P.TaskState.Name(status.state), P.TaskStatus.Reason.Name(status.reason))
             set_permanently_failed(self.state_store, [info])

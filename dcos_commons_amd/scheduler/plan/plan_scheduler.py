@@ -4,6 +4,12 @@ Reference: sdk/.../scheduler/plan/PlanScheduler.java:27-166. For each candidate 
 ``step.start()``, kill the live tasks sharing the resource sets about to be relaunched, run the
 ``OfferEvaluator``, hand the recommendations to the step, and remove consumed offers before the
 next step (greedy).
+
+Difference from the reference: the reference evaluates every step of a cycle against the task set
+stored before the cycle, so placement rules that count tasks (``MAX_PER`` zone/region/attribute,
+``GROUP_BY``, task-type avoid/colocate) cannot see pods matched earlier in the same cycle and a
+parallel phase can over-place. Here each matched step's TaskInfos join the snapshot before the next
+step is evaluated (with or without launch streaming).
 """
 from __future__ import annotations
 
@@ -11,6 +17,7 @@ import logging
 from typing import List, Optional
 
 from dcos_commons_amd.framework import task_killer
+from dcos_commons_amd.offer.recommendations import StoreTaskInfoRecommendation
 from dcos_commons_amd.offer.task_utils import is_terminal
 from dcos_commons_amd.utils.logging_utils import get_logger
 
@@ -28,8 +35,8 @@ class PlanScheduler:
         step is matched (launch streaming); its return value replaces them in the result."""
         all_recs = []
         available = list(offers)
-        # Launches are only recorded after the whole cycle (write-ahead, then ACCEPT), so the
-        # stored task set is constant across the steps of one cycle: read it once.
+        # Read the stored task set once per cycle; the TaskInfos of each matched step are merged
+        # into it, so later steps see the pods placed earlier in this cycle.
         all_tasks = {t.name: t for t in self.state_store.fetch_tasks()} if steps else {}
         for step in steps:
             recs = self._step_offers(available, step, all_tasks)
@@ -37,6 +44,9 @@ class PlanScheduler:
                 used = {r.offer_id.value for r in recs}
                 if on_step is not None:
                     recs = on_step(recs)
+                for r in recs:
+                    if isinstance(r, StoreTaskInfoRecommendation) and r.task_info.task_id.value:
+                        all_tasks[r.task_info.name] = r.state_store_task_info()
                 all_recs.extend(recs)
                 available = [o for o in available if o.id.value not in used]
         return all_recs

@@ -274,10 +274,14 @@ class SchedulerConfig:
 
     def is_unknown_as_lost(self) -> bool:
         """Trust the master's "never heard of this task": a reconciliation TASK_UNKNOWN is handled as
-        TASK_LOST so the task is recovered, and a launch the master reports LOST/DROPPED while our
-        only record is the write-ahead STAGING status is relaunched with fresh reservations
-        (reference: the UNKNOWN status is stored and never recovered, and such a launch waits
-        forever for reservations that were never made)."""
+        TASK_LOST so the task is recovered (in place: a TRANSIENT recovery on the task's existing
+        reservations), and a *first-footprint* launch (stored TaskInfo labelled
+        ``launch_new_footprint``, i.e. every reservation it references was created by that launch)
+        that the master reports LOST/DROPPED while our only record is the write-ahead STAGING
+        status is relaunched with fresh reservations. An in-place relaunch never is: its
+        reservations and volumes exist regardless of the lost ACCEPT (reference: the UNKNOWN status
+        is stored and never recovered, and a lost first launch waits forever for reservations that
+        were never made)."""
         return self.env.get_optional_boolean("SDK_UNKNOWN_AS_LOST", True)
 
     def implicit_reconcile_delay_s(self) -> float:

@@ -4,6 +4,11 @@ Reference: sdk/.../state/PersistentLaunchRecorder.java:32-212. Every ``StoreTask
 is persisted *before* the ACCEPT is sent (empty-TaskID entries first), together with a synthetic
 ``TASK_STAGING`` status for real launches; tasks sharing a resource set with the launched task get
 the new resources copied onto their stored TaskInfo.
+
+Addition: a launch whose TaskInfo references only reservations that no stored task of its pod
+instance referenced before this batch created its whole footprint (first launch or permanent
+replace). Its stored TaskInfo carries ``launch_new_footprint=true``; an in-place relaunch that
+reuses existing reservations or volumes never does.
 """
 from __future__ import annotations
 
@@ -13,7 +18,8 @@ from typing import Optional
 from dcos_commons_amd.mesos import protos as P
 from dcos_commons_amd.offer import task_utils
 from dcos_commons_amd.offer.recommendations import StoreTaskInfoRecommendation
-from dcos_commons_amd.offer.taskdata.labels import TaskException, TaskLabelReader
+from dcos_commons_amd.offer.resources import get_all_resources, get_resource_ids
+from dcos_commons_amd.offer.taskdata.labels import TaskException, TaskLabelReader, TaskLabelWriter
 from dcos_commons_amd.specification.specs import PodInstance
 
 
@@ -26,15 +32,26 @@ class PersistentLaunchRecorder:
     def record(self, recommendations) -> None:
         stores = [r for r in recommendations if isinstance(r, StoreTaskInfoRecommendation)]
         stores.sort(key=lambda r: len(r.task_info.task_id.value))
-        for rec in stores:
-            info = rec.state_store_task_info()
+        infos = [rec.state_store_task_info() for rec in stores]
+        # reservations the pod instances of this batch referenced before any of it is written
+        prior_ids = {}
+        for info in infos:
+            if info.task_id.value == "":
+                continue
+            pi = self._pod_instance(info)
+            if pi is not None and pi.name not in prior_ids:
+                prior_ids[pi.name] = self._stored_resource_ids(pi)
+        for info in infos:
             status = None
+            pi = self._pod_instance(info)
             if info.task_id.value != "":
                 status = P.TaskStatus(state=P.TASK_STAGING)
                 status.task_id.CopyFrom(info.task_id)
                 if info.HasField("executor"):
                     status.executor_id.CopyFrom(info.executor.executor_id)
-            pi = self._pod_instance(info)
+                ids = get_resource_ids(get_all_resources(info))
+                new = bool(ids) and pi is not None and not (set(ids) & prior_ids.get(pi.name, set()))
+                TaskLabelWriter(info).set_launch_new_footprint(new).apply()
             if pi is not None:
                 self._update_resource_set_peers(pi, info)
             self.state_store.store_tasks([info])
@@ -47,6 +64,14 @@ class PersistentLaunchRecorder:
             return PodInstance(pod, TaskLabelReader(info).get_index()) if pod is not None else None
         except (TaskException, ValueError):
             return None
+
+    def _stored_resource_ids(self, pi: PodInstance) -> set:
+        out = set()
+        for t in pi.pod.tasks:
+            stored = self.state_store.fetch_task(f"{pi.name}-{t.name}")
+            if stored is not None:
+                out.update(get_resource_ids(get_all_resources(stored)))
+        return out
 
     def _update_resource_set_peers(self, pi: PodInstance, info: P.TaskInfo) -> None:
         spec = task_utils.get_task_spec(pi, info.name)

@@ -213,3 +213,74 @@ def test_task_forgotten_reference_behaviour_never_recovers():
         c.wait(lambda: c.state("world-1-server") == P.TASK_UNKNOWN, what="TASK_UNKNOWN stored")
         time.sleep(0.5)
         assert c.task_id("world-1-server") == tid
+
+
+def _restart_pod_with_lost_accept(c, pod):
+    """Restart ``pod`` in place while its relaunch ACCEPT is lost in transit."""
+    c.master.drop_next_accepts(1)
+    assert c.api.post(f"/v1/pod/{pod}/restart").status == 200
+    c.wait(lambda: c.master.dropped_accepts == 1, what="relaunch ACCEPT dropped")
+
+
+def test_lost_accept_on_in_place_relaunch_keeps_the_volume():
+    """the relaunch of a pod that already owns reservations and a persistent
+    volume must stay TRANSIENT when its ACCEPT is lost (the watchdog's reconciliation answers
+    LOST/UNKNOWN): same agent, same volume, never marked permanently failed."""
+    from dcos_commons_amd.offer.taskdata.labels import TaskLabelReader
+
+    with Chaos() as c:
+        c.wait_plan("deploy")
+        name = "hello-0-server"
+        tid, aid, vols = c.task_id(name), c.agent_of(name), _volume_ids(c, name)
+        assert vols
+        assert TaskLabelReader(c.store.fetch_task(name)).is_launch_new_footprint()   # first launch
+        _restart_pod_with_lost_accept(c, "hello-0")
+        c.wait(lambda: c.task_id(name) != tid and c.state(name) == P.TASK_RUNNING
+               and c.task_id(name) in c.running_ids(), timeout=30, what="hello-0 relaunched")
+        info = c.store.fetch_task(name)
+        assert not TaskLabelReader(info).is_permanently_failed()
+        assert not TaskLabelReader(info).is_launch_new_footprint()                   # in-place relaunch
+        assert c.agent_of(name) == aid
+        assert _volume_ids(c, name) == vols
+
+
+def _stage_relaunch(c, name, new_footprint):
+    """Write-ahead state of a relaunch whose ACCEPT never reached the master."""
+    from dcos_commons_amd.offer.taskdata.labels import TaskLabelWriter
+
+    info = P.TaskInfo()
+    info.CopyFrom(c.store.fetch_task(name))
+    info.task_id.value = info.task_id.value + "-relaunch"
+    TaskLabelWriter(info).set_launch_new_footprint(new_footprint).apply()
+    c.store.store_tasks([info])
+    staging = P.TaskStatus(state=P.TASK_STAGING)
+    staging.task_id.CopyFrom(info.task_id)
+    c.store.store_status(name, staging)
+    return info
+
+
+def _master_reply(info, state, reason):
+    st = P.TaskStatus(state=state, source=P.TaskStatus.SOURCE_MASTER, reason=reason)
+    st.task_id.CopyFrom(info.task_id)
+    return st
+
+
+def test_never_launched_rule_applies_only_to_a_new_footprint():
+    """The never-launched rule (TASK_DROPPED/REASON_INVALID_OFFERS or reconciliation LOST on the
+    write-ahead STAGING status) re-footprints a first launch, and never an in-place relaunch."""
+    from dcos_commons_amd.offer.taskdata.labels import TaskLabelReader
+
+    cases = [(P.TASK_DROPPED, P.TaskStatus.REASON_INVALID_OFFERS),
+             (P.TASK_LOST, P.TaskStatus.REASON_RECONCILIATION)]
+    with Chaos() as c:
+        c.wait_plan("deploy")
+        sched = c.runner.scheduler
+        for state, reason in cases:
+            # relaunch in place: reservations exist, the task must stay transiently failed
+            info = _stage_relaunch(c, "world-0-server", new_footprint=False)
+            sched.process_status_update(_master_reply(info, state, reason))
+            assert not TaskLabelReader(c.store.fetch_task("world-0-server")).is_permanently_failed()
+        # first footprint: the reservations were never made, so it is re-footprinted
+        info = _stage_relaunch(c, "world-1-server", new_footprint=True)
+        sched.process_status_update(_master_reply(info, P.TASK_DROPPED, P.TaskStatus.REASON_INVALID_OFFERS))
+        assert TaskLabelReader(c.store.fetch_task("world-1-server")).is_permanently_failed()

@@ -125,3 +125,16 @@ def test_gpu_health_reports_healthy(dev):
     assert rep["healthy"], rep
     r2 = gpu_health.readiness_probe(0)
     assert r2["healthy"], r2
+
+
+def test_readiness_probe_on_a_non_default_device(dev):
+    """the readiness probe must make its device current before launching (the HIP
+    kernels run on the current device's stream)."""
+    from dcos_commons_amd.ops.gpu_health import readiness_probe
+
+    if torch.cuda.device_count() < 2:
+        pytest.skip("needs a second visible GPU")
+    torch.cuda.set_device(0)
+    rep = readiness_probe(1)
+    assert rep["healthy"], rep
+    assert torch.cuda.current_device() == 0       # the caller's current device is restored

@@ -502,3 +502,58 @@ def test_resource_pool_consume_reserved_by_id():
     v.scalar.value = 1.0
     assert pool.consume_reserved("cpus", v, rid) is not None
     assert pool.consume_reserved("cpus", v, rid) is None       # consumed once
+
+
+# ---------------------------------------------------------------------------------------
+# write-ahead footprint marker (launch_new_footprint) and same-cycle placement
+
+
+def test_recorder_marks_only_launches_that_create_their_footprint():
+    f = Fixture(server(1.0, 32, extra="volume:\n  path: data\n  type: ROOT\n  size: 10\n"))
+    first = f.launch([complete_offer(scalar("cpus", 2.0), scalar("mem", 64), scalar("disk", 64))])
+    assert TaskLabelReader(f.task()).is_launch_new_footprint()
+    # relaunch in place on the reservations + volume the first launch created
+    reserved = _executor_reserved(first) + [r for r in of(first, LaunchOfferRecommendation)[0].task_info.resources]
+    again = f.launch([offer(*reserved)])
+    assert ops(again) == [L, None]
+    assert not TaskLabelReader(f.task()).is_launch_new_footprint()
+
+
+class _Step:
+    def __init__(self, req):
+        self.req, self.recs, self.started = req, None, False
+
+    def is_pending(self):
+        return not self.started
+
+    def is_prepared(self):
+        return False
+
+    def start(self):
+        self.started = True
+
+    def get_pod_instance_requirement(self):
+        return self.req
+
+    def update_offer_status(self, recs):
+        self.recs = recs
+
+    def get_name(self):
+        return f"step-{self.req.pod_instance.index}"
+
+
+def test_same_cycle_placement_sees_pods_matched_earlier_in_the_cycle():
+    """MAX_PER rack 1 with two pods in one offer cycle: the second step must see the first
+    step's pod (the reference evaluates both against the pre-cycle task set and can stack them)."""
+    from dcos_commons_amd.scheduler.plan.plan_scheduler import PlanScheduler
+
+    f = Fixture(server(1.0, 32), pod_extra='placement: \'[["rack", "MAX_PER", "1"]]\'\n', count=2)
+    offers = [complete_offer(scalar("cpus", 2.0), scalar("mem", 64), oid=f"o{i}", host=f"host{i}",
+                             agent=f"agent{i}", attrs=[text_attribute("rack", rack)])
+              for i, rack in ((1, "r1"), (2, "r1"), (3, "r2"))]
+    steps = [_Step(f.requirement(index=i)) for i in (0, 1)]
+    recs = PlanScheduler(f.evaluator, f.state_store).resource_offers(offers, steps)
+    launches = of(recs, LaunchOfferRecommendation)
+    assert len(launches) == 2
+    assert sorted(TaskLabelReader(l.task_info).get_offer_attribute_strings()[0] for l in launches) == \
+        ["rack:r1", "rack:r2"]
