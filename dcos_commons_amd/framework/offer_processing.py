@@ -520,6 +520,15 @@ class OfferProcessor:
                 if self._check_status():
                     self._evaluate(offers, now)
                     sp.set(working=True)
+                    if getattr(self.client, "consume_recheck_request", None) is not None and \
+                            self.client.consume_recheck_request():
+                        # the client started work that changes its status (e.g. uninstall's
+                        # deregister step): re-check now rather than at the next offer poll
+                        self._wake.set()
+                elif self._deregistered:
+                    # the framework was just torn down: its offers went with it
+                    self._held.clear()
+                    return
                 elif offers:
                     self._held.clear()
                     if self.gc_all_offers:

@@ -8,7 +8,9 @@ from __future__ import annotations
 import faulthandler
 import logging
 import os
+import signal
 import sys
+import threading
 
 LOGGER = logging.getLogger(__name__)
 
@@ -52,5 +54,47 @@ class ProcessExit:
             faulthandler.dump_traceback(file=sys.stderr, all_threads=True)
         except Exception:  # noqa: BLE001
             pass
+        run_shutdown_hooks()
         logging.shutdown()
         os._exit(code)
+
+
+# -- shutdown hooks (the JVM's Runtime.addShutdownHook: e.g. CuratorLocker releases the service lock
+#    so the next scheduler does not wait for the ZooKeeper session to expire) ---------------------
+_hooks = []
+_hooks_lock = threading.Lock()
+_hooks_ran = False
+
+
+def add_shutdown_hook(fn) -> None:
+    with _hooks_lock:
+        _hooks.append(fn)
+
+
+def run_shutdown_hooks() -> None:
+    global _hooks_ran
+    with _hooks_lock:
+        if _hooks_ran:
+            return
+        _hooks_ran = True
+        hooks = list(reversed(_hooks))
+    for fn in hooks:
+        try:
+            fn()
+        except Exception:  # noqa: BLE001
+            LOGGER.exception("shutdown hook failed")
+
+
+def install_signal_handlers() -> bool:
+    """SIGTERM (what Marathon sends to roll or stop a scheduler) runs the shutdown hooks and exits
+    with 143, as the JVM does. Only possible from the main thread; returns whether installed."""
+    if threading.current_thread() is not threading.main_thread():
+        return False
+
+    def on_term(signum, frame):
+        LOGGER.info("Received signal %d: running shutdown hooks and exiting", signum)
+        run_shutdown_hooks()
+        logging.shutdown()
+        os._exit(128 + signum)
+    signal.signal(signal.SIGTERM, on_term)
+    return True

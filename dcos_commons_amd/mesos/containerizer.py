@@ -1,0 +1,417 @@
+"""Real-process task runtime for the in-process agents of ``LocalMaster``.
+
+The synthetic ``TaskBehavior`` only moves task states along a timeline. ``ProcessTaskBehavior``
+makes each agent behave like a Mesos agent with the Mesos containerizer and the default executor:
+
+* **sandbox** per task: ``<work>/<agent host>/frameworks/<fw>/executors/<executor>/tasks/<task id>``
+  with ``stdout``/``stderr`` files; ``CommandInfo.uris`` are fetched into it (local paths and
+  loopback ``http://`` URLs; anything else is skipped, there is no network);
+* **persistent volumes** (``disk.persistence`` on the task's or its executor's resources) live in
+  ``<work>/<agent host>/volumes/<persistence id>`` and are linked into the sandbox at their
+  ``container_path``, so data survives relaunches on the same reservation and is deleted by a
+  ``DESTROY``; host-path and sandbox-path container volumes are linked too; secret volumes and
+  secret env vars are resolved through ``secret_resolver``;
+* **environment**: the task's ``CommandInfo.environment`` plus ``MESOS_SANDBOX``/``MESOS_TASK_ID``
+  and friends, and ``HIP_VISIBLE_DEVICES``/``ROCR_VISIBLE_DEVICES`` from the GPU devices the agent
+  assigned (what the Mesos GPU isolator does for a task that asked for ``gpus``);
+* **lifecycle**: ``bash -c <cmd>`` in its own session; exit 0 -> ``TASK_FINISHED``, otherwise
+  ``TASK_FAILED``; a scheduler KILL sends SIGTERM to the session and SIGKILL after the task's
+  ``kill_policy`` grace period -> ``TASK_KILLED``;
+* **checks**: the readiness ``check`` command runs in the sandbox (``LocalMaster``'s check loop);
+  the ``health_check`` command runs every ``interval_seconds`` after ``delay_seconds``; health
+  changes are reported on ``TASK_RUNNING`` updates and ``consecutive_failures`` failures past the
+  grace period kill the task (``TASK_KILLED``, ``healthy=false``).
+
+Test hooks: ``exec_in_task`` (``dcos task exec``), ``kill_with_pattern`` (``pkill -9 -f`` limited
+to the sessions this runtime started) and ``sandbox_of``. Every process this runtime starts is in a
+session it owns; ``shutdown()`` kills them all.
+"""
+from __future__ import annotations
+
+import logging
+import os
+import re
+import shutil
+import signal
+import subprocess
+import threading
+import time
+import urllib.parse
+import urllib.request
+from dataclasses import dataclass, field
+from typing import Callable, Dict, List, Optional, Tuple
+
+from dcos_commons_amd.mesos import protos as P
+from dcos_commons_amd.mesos.local_master import TaskBehavior, TaskTiming
+
+LOGGER = logging.getLogger(__name__)
+_LOOPBACK = {"127.0.0.1", "localhost", "::1"}
+DEFAULT_KILL_GRACE_S = 3.0
+
+
+@dataclass
+class _Proc:
+    task_id: str
+    name: str
+    agent_host: str
+    sandbox: str
+    env: Dict[str, str]
+    popen: Optional[subprocess.Popen] = None
+    killed: bool = False
+    unhealthy: bool = False
+    health_stop: threading.Event = field(default_factory=threading.Event)
+    exited: threading.Event = field(default_factory=threading.Event)
+    rc: Optional[int] = None
+
+
+def _safe(name: str) -> str:
+    return re.sub(r"[^A-Za-z0-9_.-]", "_", name) or "_"
+
+
+def _session_pids(sid: int) -> List[int]:
+    """Live processes whose session id is ``sid`` (the task's own session)."""
+    out = []
+    for d in os.listdir("/proc"):
+        if not d.isdigit():
+            continue
+        try:
+            with open(f"/proc/{d}/stat", "rb") as f:
+                stat = f.read().decode("utf-8", "replace")
+            # fields after the ")" that closes comm: state ppid pgrp session ...
+            rest = stat[stat.rindex(")") + 2:].split()
+            if int(rest[3]) == sid:
+                out.append(int(d))
+        except (OSError, ValueError, IndexError):
+            continue
+    return out
+
+
+def _cmdline(pid: int) -> str:
+    try:
+        with open(f"/proc/{pid}/cmdline", "rb") as f:
+            return f.read().replace(b"\0", b" ").decode("utf-8", "replace").strip()
+    except OSError:
+        return ""
+
+
+class ProcessTaskBehavior(TaskBehavior):
+    executes_commands = True
+
+    def __init__(self, work_dir: str, secret_resolver: Optional[Callable[[str], Optional[bytes]]] = None,
+                 default_kill_grace_s: float = DEFAULT_KILL_GRACE_S, extra_env: Optional[Dict[str, str]] = None,
+                 check_workers: int = 8, resolver: Optional[Callable[[str], Optional[str]]] = None):
+        """``resolver(hostname)`` maps cluster DNS names to an address the fetcher can reach
+        (``None``: not a cluster name)."""
+        super().__init__(default=TaskTiming(), check_runner=self._run_readiness_check, check_workers=check_workers)
+        self.work_dir = os.path.abspath(work_dir)
+        os.makedirs(self.work_dir, exist_ok=True)
+        self.secret_resolver = secret_resolver
+        self.resolver = resolver
+        self.default_kill_grace_s = default_kill_grace_s
+        self.extra_env = dict(extra_env or {})
+        self._procs: Dict[str, _Proc] = {}
+        self._lock = threading.Lock()
+
+    # -- paths -----------------------------------------------------------------------
+    def _agent_dir(self, host: str) -> str:
+        return os.path.join(self.work_dir, _safe(host))
+
+    def volume_dir(self, host: str, persistence_id: str) -> str:
+        return os.path.join(self._agent_dir(host), "volumes", _safe(persistence_id))
+
+    def mount_dir(self, host: str, root: str) -> str:
+        return os.path.join(self._agent_dir(host), "mounts", _safe(root.strip("/")))
+
+    def sandbox_of(self, task_id: str) -> Optional[str]:
+        with self._lock:
+            p = self._procs.get(task_id)
+        return p.sandbox if p is not None else None
+
+    # -- launch (called on the master's actor thread) --------------------------------
+    def launch(self, master, task, agent) -> None:
+        info: P.TaskInfo = task.info
+        host = agent.spec.hostname
+        eid = task.executor_id or "command"
+        sandbox = os.path.join(self._agent_dir(host), "frameworks", _safe(task.framework_id), "executors",
+                               _safe(eid), "tasks", _safe(info.task_id.value))
+        os.makedirs(sandbox, exist_ok=True)
+        proc = _Proc(info.task_id.value, info.name, host, sandbox, {})
+        with self._lock:
+            self._procs[proc.task_id] = proc
+        try:
+            self._link_volumes(host, sandbox, list(info.resources) + self._executor_resources(master, task, agent))
+            self._link_container_volumes(sandbox, info)
+            self._fetch(sandbox, info.command.uris)
+            proc.env = self._environment(master, task, agent, sandbox)
+            with open(os.path.join(sandbox, "stdout"), "ab") as out, open(os.path.join(sandbox, "stderr"), "ab") as err:
+                proc.popen = subprocess.Popen(["bash", "-c", info.command.value or "true"], cwd=sandbox,
+                                              env=proc.env, stdin=subprocess.DEVNULL, stdout=out, stderr=err,
+                                              start_new_session=True)
+        except Exception as e:  # noqa: BLE001
+            LOGGER.exception("failed to start %s", info.name)
+            master._schedule(0, master._container_failed, task, task.epoch, str(e))
+            proc.exited.set()
+            return
+        epoch = task.epoch
+        threading.Thread(target=self._wait, args=(master, task, epoch, proc), name=f"wait-{info.name}",
+                         daemon=True).start()
+        master._schedule(0, master._lifecycle_starting, task, epoch, self.timing(info))
+
+    @staticmethod
+    def _executor_resources(master, task, agent) -> List[P.Resource]:
+        e = agent.executors.get((task.framework_id, task.executor_id))
+        return list(e.info.resources) if e is not None else []
+
+    def _link(self, target: str, sandbox: str, container_path: str) -> None:
+        if not container_path or os.path.isabs(container_path):
+            return  # absolute container paths need a mount namespace: not modelled
+        link = os.path.join(sandbox, container_path)
+        os.makedirs(os.path.dirname(link), exist_ok=True)
+        if os.path.lexists(link):
+            return
+        os.symlink(target, link)
+
+    def _link_volumes(self, host: str, sandbox: str, resources: List[P.Resource]) -> None:
+        for r in resources:
+            if not r.HasField("disk") or not r.disk.HasField("persistence") or not r.disk.persistence.id:
+                continue
+            if r.disk.HasField("source") and r.disk.source.type == P.Resource.DiskInfo.Source.MOUNT:
+                target = os.path.join(self.mount_dir(host, r.disk.source.mount.root), _safe(r.disk.persistence.id))
+            else:
+                target = self.volume_dir(host, r.disk.persistence.id)
+            os.makedirs(target, exist_ok=True)
+            self._link(target, sandbox, r.disk.volume.container_path)
+
+    def _link_container_volumes(self, sandbox: str, info: P.TaskInfo) -> None:
+        for v in info.container.volumes:
+            src = v.source
+            if src.type == P.Volume.Source.SECRET:
+                data = self._secret(src.secret)
+                path = os.path.join(sandbox, v.container_path)
+                os.makedirs(os.path.dirname(path), exist_ok=True)
+                with open(path, "wb") as f:
+                    f.write(data or b"")
+            elif src.type == P.Volume.Source.HOST_PATH or v.host_path:
+                self._link(src.host_path.path or v.host_path, sandbox, v.container_path)
+            elif src.type == P.Volume.Source.SANDBOX_PATH:
+                target = os.path.join(sandbox, src.sandbox_path.path)
+                os.makedirs(target, exist_ok=True)
+                self._link(target, sandbox, v.container_path)
+
+    def _secret(self, secret: P.Secret) -> Optional[bytes]:
+        if secret.type == P.Secret.VALUE:
+            return secret.value.data
+        if self.secret_resolver is None:
+            return None
+        return self.secret_resolver(secret.reference.name)
+
+    def _fetch(self, sandbox: str, uris) -> None:
+        for u in uris:
+            parsed = urllib.parse.urlparse(u.value)
+            name = u.output_file or os.path.basename(parsed.path) or "download"
+            dest = os.path.join(sandbox, name)
+            addr = parsed.hostname if parsed.hostname in _LOOPBACK else (
+                self.resolver(parsed.hostname) if self.resolver is not None and parsed.hostname else None)
+            try:
+                if parsed.scheme in ("", "file"):
+                    shutil.copyfile(parsed.path, dest)
+                elif parsed.scheme in ("http", "https") and addr is not None:
+                    url = u.value.replace(parsed.hostname, addr, 1)
+                    with urllib.request.urlopen(url, timeout=10) as resp, open(dest, "wb") as f:
+                        shutil.copyfileobj(resp, f)
+                else:
+                    LOGGER.info("fetcher: skipping %s (no network in the local cluster)", u.value)
+                    continue
+            except OSError as e:
+                LOGGER.warning("fetcher: %s: %s", u.value, e)
+                continue
+            if u.executable:
+                os.chmod(dest, 0o755)
+            elif u.extract and re.search(r"\.(tar\.gz|tgz|tar|zip)$", dest):
+                try:
+                    shutil.unpack_archive(dest, sandbox)
+                except (shutil.ReadError, ValueError, OSError) as e:
+                    LOGGER.warning("fetcher: cannot extract %s: %s", dest, e)
+
+    def _environment(self, master, task, agent, sandbox: str) -> Dict[str, str]:
+        env = {k: os.environ[k] for k in ("PATH", "LANG", "LC_ALL", "TZ", "TMPDIR") if k in os.environ}
+        env.update(self.extra_env)
+        for v in task.info.command.environment.variables:
+            if v.type == P.Environment.Variable.SECRET:
+                data = self._secret(v.secret)
+                env[v.name] = data.decode("utf-8", "replace") if data is not None else ""
+            else:
+                env[v.name] = v.value
+        env.update({
+            "MESOS_SANDBOX": sandbox, "MESOS_TASK_ID": task.info.task_id.value,
+            "MESOS_FRAMEWORK_ID": task.framework_id, "MESOS_AGENT_ID": agent.id,
+            "MESOS_EXECUTOR_ID": task.executor_id, "MESOS_CONTAINER_IP": "127.0.0.1",
+            "LIBPROCESS_IP": "127.0.0.1", "HOST": agent.spec.hostname, "HOME": sandbox,
+        })
+        if task.gpu_devices:
+            devs = ",".join(str(d) for d in task.gpu_devices)
+            env["HIP_VISIBLE_DEVICES"] = devs
+            env["ROCR_VISIBLE_DEVICES"] = devs
+        return env
+
+    # -- process supervision ----------------------------------------------------------
+    def _wait(self, master, task, epoch: int, proc: _Proc) -> None:
+        rc = proc.popen.wait()
+        proc.rc = rc
+        proc.health_stop.set()
+        # a task's session may leave stragglers (e.g. `sleep &`): the container is torn down
+        self._signal_session(proc, signal.SIGKILL)
+        proc.exited.set()
+        master._schedule(0, master._process_exited, task, epoch, rc, proc.killed, proc.unhealthy)
+
+    def started(self, master, task, epoch: int) -> None:
+        """Called when the task reports RUNNING: start its health checks."""
+        hc = task.info.health_check if task.info.HasField("health_check") else None
+        if hc is None or hc.type != P.HealthCheck.COMMAND:
+            return
+        with self._lock:
+            proc = self._procs.get(task.info.task_id.value)
+        if proc is None:
+            return
+        threading.Thread(target=self._health_loop, args=(master, task, epoch, proc, hc),
+                         name=f"health-{task.info.name}", daemon=True).start()
+
+    def _health_loop(self, master, task, epoch: int, proc: _Proc, hc: P.HealthCheck) -> None:
+        t0 = time.monotonic()
+        if proc.health_stop.wait(hc.delay_seconds):
+            return
+        failures, healthy = 0, None
+        while not proc.health_stop.is_set():
+            ok = self._run_command(proc, hc.command.value, hc.timeout_seconds) == 0
+            if ok:
+                failures = 0
+            elif time.monotonic() - t0 >= hc.grace_period_seconds:
+                failures += 1
+            if ok != healthy:
+                healthy = ok
+                master._schedule(0, master._health_changed, task, epoch, ok)
+            if failures >= max(1, hc.consecutive_failures):
+                LOGGER.info("%s failed %d consecutive health checks: killing it", proc.name, failures)
+                proc.unhealthy = True
+                self._terminate(proc, self.default_kill_grace_s)
+                return
+            if proc.health_stop.wait(max(0.05, hc.interval_seconds)):
+                return
+
+    def _run_command(self, proc: _Proc, cmd: str, timeout_s: float) -> int:
+        try:
+            r = subprocess.run(["bash", "-c", cmd], cwd=proc.sandbox, env=proc.env, stdin=subprocess.DEVNULL,
+                               stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL,
+                               timeout=timeout_s if timeout_s > 0 else None, start_new_session=True)
+            return r.returncode
+        except subprocess.TimeoutExpired:
+            return 124
+        except OSError:
+            return 127
+
+    def _run_readiness_check(self, task_info: P.TaskInfo, devices) -> bool:
+        with self._lock:
+            proc = self._procs.get(task_info.task_id.value)
+        if proc is None or proc.exited.is_set():
+            return False
+        check = task_info.check
+        return self._run_command(proc, check.command.command.value, check.timeout_seconds) == 0
+
+    # -- kill ---------------------------------------------------------------------------
+    def kill(self, master, task) -> bool:
+        """Scheduler KILL: True when a live process was signalled (its exit reports KILLED)."""
+        with self._lock:
+            proc = self._procs.get(task.info.task_id.value)
+        if proc is None or proc.popen is None or proc.exited.is_set():
+            return False
+        proc.killed = True
+        grace = self.default_kill_grace_s
+        if task.info.HasField("kill_policy") and task.info.kill_policy.HasField("grace_period"):
+            grace = task.info.kill_policy.grace_period.nanoseconds / 1e9
+        self._terminate(proc, grace)
+        return True
+
+    def _signal_session(self, proc: _Proc, sig: int) -> int:
+        if proc.popen is None:
+            return 0
+        n = 0
+        for pid in _session_pids(proc.popen.pid):
+            try:
+                os.kill(pid, sig)
+                n += 1
+            except ProcessLookupError:
+                pass
+        return n
+
+    def _terminate(self, proc: _Proc, grace_s: float) -> None:
+        proc.health_stop.set()
+        self._signal_session(proc, signal.SIGTERM)
+
+        def escalate():
+            if not proc.exited.wait(max(0.0, grace_s)):
+                self._signal_session(proc, signal.SIGKILL)
+        threading.Thread(target=escalate, name=f"kill-{proc.name}", daemon=True).start()
+
+    def release(self, task) -> None:
+        """The master forgot the task (terminal, torn down, agent gone): the container goes too."""
+        with self._lock:
+            proc = self._procs.get(task.info.task_id.value)
+        if proc is not None and not proc.exited.is_set():
+            proc.killed = True
+            self._terminate(proc, 0.0)
+
+    def destroy_volumes(self, agent, volumes) -> None:
+        for v in volumes:
+            if v.HasField("disk") and v.disk.HasField("persistence") and v.disk.persistence.id:
+                if v.disk.HasField("source") and v.disk.source.type == P.Resource.DiskInfo.Source.MOUNT:
+                    path = os.path.join(self.mount_dir(agent.spec.hostname, v.disk.source.mount.root),
+                                        _safe(v.disk.persistence.id))
+                else:
+                    path = self.volume_dir(agent.spec.hostname, v.disk.persistence.id)
+                shutil.rmtree(path, ignore_errors=True)
+
+    # -- test hooks ---------------------------------------------------------------------
+    def exec_in_task(self, task_id: str, cmd: str, timeout_s: float = 30.0) -> Tuple[int, str, str]:
+        """``dcos task exec``: run ``cmd`` in the task's sandbox with its environment."""
+        with self._lock:
+            proc = self._procs.get(task_id)
+        if proc is None:
+            raise KeyError(task_id)
+        r = subprocess.run(["bash", "-c", cmd], cwd=proc.sandbox, env=proc.env, stdin=subprocess.DEVNULL,
+                           capture_output=True, timeout=timeout_s, start_new_session=True)
+        return r.returncode, r.stdout.decode("utf-8", "replace"), r.stderr.decode("utf-8", "replace")
+
+    def kill_with_pattern(self, pattern: str, agent_host: Optional[str] = None, sig: int = signal.SIGKILL) -> int:
+        """``pkill -<sig> -f <pattern>`` over the processes of the tasks this runtime started
+        (optionally only on one agent). Returns how many processes were signalled."""
+        rx = re.compile(pattern)
+        with self._lock:
+            procs = [p for p in self._procs.values() if not p.exited.is_set()
+                     and (agent_host is None or p.agent_host == agent_host)]
+        n = 0
+        for p in procs:
+            if p.popen is None:
+                continue
+            for pid in _session_pids(p.popen.pid):
+                if rx.search(_cmdline(pid)):
+                    try:
+                        os.kill(pid, sig)
+                        n += 1
+                    except ProcessLookupError:
+                        pass
+        return n
+
+    def running_task_ids(self) -> List[str]:
+        with self._lock:
+            return [t for t, p in self._procs.items() if not p.exited.is_set()]
+
+    def shutdown(self) -> None:
+        with self._lock:
+            procs = list(self._procs.values())
+        for p in procs:
+            if not p.exited.is_set():
+                p.killed = True
+                p.health_stop.set()
+                self._signal_session(p, signal.SIGKILL)
+        for p in procs:
+            p.exited.wait(5.0)

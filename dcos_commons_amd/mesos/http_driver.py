@@ -98,6 +98,7 @@ class V1HttpSchedulerDriver(SchedulerDriver):
         self._conns: List[http.client.HTTPConnection] = []
         self._conns_lock = threading.Lock()
         self.exit_status = 0
+        self._tearing_down = False
 
     # -- lifecycle ---------------------------------------------------------------------
     @property
@@ -124,7 +125,7 @@ class V1HttpSchedulerDriver(SchedulerDriver):
     def stop(self, failover: bool = True) -> None:
         if self._stopped.is_set():
             return
-        if not failover and self._framework_id and self.stream_id:
+        if not failover and self._framework_id and self.stream_id and not self._tearing_down:
             try:
                 self._send(P.Call(type=P.Call.TEARDOWN))
             except Exception as e:  # noqa: BLE001
@@ -195,6 +196,8 @@ class V1HttpSchedulerDriver(SchedulerDriver):
         self._send(call)
 
     def teardown(self) -> None:
+        # the master ends the event stream in answer: that is not a disconnection
+        self._tearing_down = True
         self._send(P.Call(type=P.Call.TEARDOWN))
 
     # -- transport ---------------------------------------------------------------------
@@ -313,7 +316,8 @@ class V1HttpSchedulerDriver(SchedulerDriver):
             self.stream_id = None
             self._subscribed.clear()
             self._close_stream()
-            if self._stopped.is_set():
+            if self._stopped.is_set() or self._tearing_down:
+                self._stopped.set()
                 return
             LOGGER.warning("Lost Mesos event stream (%s)", reason)
             if self._subscribed_once and not self.reconnect:

@@ -18,6 +18,8 @@ import argparse
 import json
 import logging
 import queue
+import select
+import socket
 import sys
 import threading
 import time
@@ -33,6 +35,7 @@ from dcos_commons_amd.mesos.local_master import AgentSpec, LocalMaster, TERMINAL
 
 LOGGER = logging.getLogger(__name__)
 _CLOSE = object()
+_PEER_POLL_S = 0.25
 
 
 class _EventSink:
@@ -168,7 +171,9 @@ class HttpMaster:
         info = call.subscribe.framework_info
         fid = info.id.value if info.HasField("id") else ""
         with self._lock:
-            old = self.subscriptions.get(fid) if fid else None
+            # unbind the old stream now: when its handler notices the close it must not disconnect
+            # the framework, which by then belongs to this new subscription
+            old = self.subscriptions.pop(fid, None) if fid else None
         if old is not None:
             old.scheduler.error(None, "Framework failed over")
             old.close()
@@ -297,6 +302,13 @@ class _Handler(BaseHTTPRequestHandler):
         status = self.owner.handle(call, self.headers.get(STREAM_ID_HEADER))
         self._reply(status, b"" if status == 202 else b"Call rejected: missing or stale Mesos-Stream-Id")
 
+    def _peer_closed(self) -> bool:
+        try:
+            r, _, _ = select.select([self.connection], [], [], 0)
+            return bool(r) and self.connection.recv(1, socket.MSG_PEEK) == b""
+        except (OSError, ValueError):
+            return True
+
     def _stream(self, call: P.Call, accept: str) -> None:
         sub = self.owner.subscribe(call, accept)
         self.send_response(200)
@@ -306,10 +318,20 @@ class _Handler(BaseHTTPRequestHandler):
         self.end_headers()
         bound = False
         try:
+            idle_s = 0.0
             while True:
                 try:
-                    ev = sub.queue.get(timeout=sub.heartbeat_s)
+                    ev = sub.queue.get(timeout=_PEER_POLL_S)
+                    idle_s = 0.0
                 except queue.Empty:
+                    # a scheduler that died closes its connection: notice it now, like Mesos does,
+                    # instead of at the next write
+                    if self._peer_closed():
+                        break
+                    idle_s += _PEER_POLL_S
+                    if idle_s < sub.heartbeat_s:
+                        continue
+                    idle_s = 0.0
                     ev = P.Event(type=P.Event.HEARTBEAT)
                 if ev is _CLOSE:
                     break

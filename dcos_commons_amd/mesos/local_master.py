@@ -224,6 +224,8 @@ class LocalMaster:
                  clock: Callable[[], float] = time.monotonic):
         self.allocation_interval_s = allocation_interval_s
         self.behavior = behavior or TaskBehavior()
+        # ProcessTaskBehavior (mesos.containerizer) runs task commands for real
+        self._executes = bool(getattr(self.behavior, "executes_commands", False))
         self.domain = domain
         self.offer_timeout_s = offer_timeout_s
         self.clock = clock
@@ -288,6 +290,9 @@ class LocalMaster:
             self._cond.notify_all()
         if threading.current_thread() is not self._thread:
             self._thread.join(timeout=5)
+        stop = getattr(self.behavior, "shutdown", None)
+        if callable(stop):
+            stop()
 
     def add_status_listener(self, fn: Callable[[str, P.TaskStatus], None]) -> None:
         self._listeners.append(fn)
@@ -681,6 +686,8 @@ class LocalMaster:
                 trial.subtract(c)
                 trial.add(strip_volume(c))
             bag._q, bag._proto = trial._q, trial._proto
+            if self._executes:
+                self.behavior.destroy_volumes(agent, op.destroy.volumes)
         elif op.type == T.LAUNCH_GROUP:
             self._launch_group(fw, agent, bag, op.launch_group.executor, list(op.launch_group.task_group.tasks))
         elif op.type == T.LAUNCH:
@@ -729,8 +736,11 @@ class LocalMaster:
             agent.tasks[t.task_id.value] = task
             if eid:
                 agent.executors[key].tasks.add(t.task_id.value)
-            timing = self.behavior.timing(t)
-            self._schedule(timing.starting_s, self._lifecycle_starting, task, task.epoch, timing)
+            if self._executes:
+                self.behavior.launch(self, task, agent)
+            else:
+                timing = self.behavior.timing(t)
+                self._schedule(timing.starting_s, self._lifecycle_starting, task, task.epoch, timing)
 
     # -- task lifecycle ----------------------------------------------------------------
     def _lifecycle_starting(self, task: _Task, epoch: int, timing: TaskTiming) -> None:
@@ -748,16 +758,18 @@ class LocalMaster:
             cs = P.CheckStatusInfo(type=info.check.type)
             cs.command.SetInParent()
             extra["check_status"] = cs
-        if info.HasField("health_check"):
+        if info.HasField("health_check") and not self._executes:
             extra["healthy"] = True
         self._update(task, P.TASK_RUNNING, **extra)
+        if self._executes:
+            self.behavior.started(self, task, epoch)
         if info.HasField("check"):
             delay = (info.check.delay_seconds if timing.honor_check_delays else 0.0) + timing.check_exec_s
             if self._check_runner(task) is not None:
                 self._schedule(delay, self._run_check, task, epoch)
             else:
                 self._schedule(delay, self._lifecycle_ready, task, epoch)
-        if timing.finish_after_s is not None:
+        if timing.finish_after_s is not None and not self._executes:
             self._schedule(timing.finish_after_s, self._lifecycle_exit, task, epoch, timing.exit_state)
 
     def _check_runner(self, task: _Task):
@@ -801,13 +813,45 @@ class LocalMaster:
         cs.command.exit_code = 0
         extra = {"check_status": cs, "reason": P.TaskStatus.REASON_TASK_CHECK_STATUS_UPDATED}
         if task.info.HasField("health_check"):
-            extra["healthy"] = True
+            if not self._executes:
+                extra["healthy"] = True
+            elif task.status.HasField("healthy"):
+                extra["healthy"] = task.status.healthy
         self._update(task, P.TASK_RUNNING, **extra)
 
     def _lifecycle_exit(self, task: _Task, epoch: int, state: int) -> None:
         if task.epoch != epoch or task.status.state in TERMINAL:
             return
         self._update(task, state, message="task exited")
+
+    # -- real-process runtime callbacks (ProcessTaskBehavior) ----------------------------
+    def _process_exited(self, task: _Task, epoch: int, rc: int, killed: bool, unhealthy: bool) -> None:
+        if task.epoch != epoch or task.status.state in TERMINAL:
+            return
+        if unhealthy:
+            self._update(task, P.TASK_KILLED, healthy=False, reason=P.TaskStatus.REASON_TASK_HEALTH_CHECK_STATUS_UPDATED,
+                         message="Task was killed since health check failed")
+        elif killed:
+            self._update(task, P.TASK_KILLED, message="Command terminated with signal SIGTERM")
+        elif rc == 0:
+            self._update(task, P.TASK_FINISHED, message="Command exited with status 0")
+        else:
+            msg = f"Command terminated with signal {-rc}" if rc < 0 else f"Command exited with status {rc}"
+            self._update(task, P.TASK_FAILED, message=msg, reason=P.TaskStatus.REASON_COMMAND_EXECUTOR_FAILED)
+
+    def _health_changed(self, task: _Task, epoch: int, healthy: bool) -> None:
+        if task.epoch != epoch or task.status.state != P.TASK_RUNNING:
+            return
+        extra = {"healthy": healthy, "reason": P.TaskStatus.REASON_TASK_HEALTH_CHECK_STATUS_UPDATED}
+        if task.status.HasField("check_status"):
+            extra["check_status"] = task.status.check_status
+        self._update(task, P.TASK_RUNNING, **extra)
+
+    def _container_failed(self, task: _Task, epoch: int, message: str) -> None:
+        if task.epoch != epoch or task.status.state in TERMINAL:
+            return
+        self._update(task, P.TASK_FAILED, message=f"Failed to launch container: {message}",
+                     reason=P.TaskStatus.REASON_CONTAINER_LAUNCH_FAILED)
 
     def _kill(self, fid: str, task_id: str) -> None:
         t = self._find_task(task_id)
@@ -833,6 +877,8 @@ class LocalMaster:
             if fw is not None:
                 fw.driver._deliver(lambda s, d=fw.driver: s.status_update(d, st))
             return
+        if self._executes and self.behavior.kill(self, t):
+            return  # TASK_KILLED is reported when the process has exited
         self._update(t, P.TASK_KILLED, message="Task killed by scheduler")
 
     def _find_task(self, task_id: str) -> Optional[_Task]:
@@ -872,6 +918,8 @@ class LocalMaster:
             fw.driver._deliver(lambda s, d=fw.driver, st=st: s.status_update(d, st))
 
     def _release_task(self, task: _Task) -> None:
+        if self._executes:
+            self.behavior.release(task)
         a = self.agents.get(task.agent_id)
         if a is None:
             return

@@ -535,6 +535,10 @@ class MultiServiceRunner:
         self.framework_runner = FrameworkRunner(self.scheduler_config, self.framework_config, self.using_gpus,
                                                 self.scheduler_config.is_region_awareness_enabled(),
                                                 driver_factory=self.driver_factory)
+        if block:
+            from dcos_commons_amd.framework.process_exit import install_signal_handlers
+
+            install_signal_handlers()
         return self.framework_runner.start(self.persister, self.client, block=block)
 
     def stop(self) -> None:

@@ -49,6 +49,10 @@ class SchedulerRunner:
             service_requests_gpu_resources(spec), self.builder.is_region_awareness_enabled(),
             driver_factory=self.driver_factory)
         self.scheduler = self.builder.build()
+        if block:
+            from dcos_commons_amd.framework.process_exit import install_signal_handlers
+
+            install_signal_handlers()
         return self.framework_runner.start(persister, self.scheduler, block=block)
 
     def stop(self) -> None:

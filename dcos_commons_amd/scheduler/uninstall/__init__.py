@@ -300,7 +300,15 @@ class UninstallScheduler:
             return OfferResponse.not_ready([])
         for s in self._candidates:
             s.start()
+            if s is self.deregister_step and s.is_running():
+                self._recheck = True
         return OfferResponse.processed([])
+
+    def consume_recheck_request(self) -> bool:
+        """True once after the deregister step started: the offer loop re-checks the client
+        status immediately and tears the framework down without waiting for the next poll."""
+        r, self._recheck = getattr(self, "_recheck", False), False
+        return r
 
     def get_unexpected_resources(self, unused_offers) -> UnexpectedResourcesResponse:
         unexpected = [OfferResources(o, [r for r in o.resources if has_resource_id(r)]) for o in unused_offers]

@@ -9,6 +9,8 @@ Backends here (``SDK_PERSISTER``):
 * ``mem`` -- in-memory, for tests and benchmarks;
 * ``zk`` -- ZooKeeper at the spec's ``scheduler.zookeeper`` / ``FRAMEWORK_ZOOKEEPER``
   (``storage.zk_persister``), optional digest credentials ``SDK_ZK_USERNAME``/``SDK_ZK_PASSWORD``.
+  ``SDK_ZOOKEEPER`` replaces the connect string where the spec's default (``master.mesos:2181``)
+  does not resolve, e.g. the local cluster of ``dcos_commons_amd.testing.cluster``.
 
 Like ``CuratorPersister.Builder.build`` (:480-520) the durable backends first take the
 single-scheduler lock (``ZkLocker`` / ``FileLocker``; ``SDK_DISABLE_LOCK=true`` skips it, for tests)
@@ -99,7 +101,8 @@ def persister_for_service(service_spec, scheduler_config) -> Persister:
     elif kind == "zk":
         from .zk_persister import ZkLocker, ZooKeeperPersister, init_service_name
 
-        connect = service_spec.zookeeper_connection or "127.0.0.1:2181"
+        connect = (env.get_optional("SDK_ZOOKEEPER", "") or service_spec.zookeeper_connection
+                   or "127.0.0.1:2181")
         user, pw = env.get_optional("SDK_ZK_USERNAME", ""), env.get_optional("SDK_ZK_PASSWORD", "")
         if lock_enabled and ZkLocker._instance is None:
             ZkLocker.lock(service_spec.name, connect, username=user, password=pw)

@@ -285,6 +285,9 @@ class ZkLocker:
                 return None
             cls._instance = inst
             atexit.register(cls.unlock)
+            from dcos_commons_amd.framework.process_exit import add_shutdown_hook
+
+            add_shutdown_hook(cls.unlock)
             return inst
 
     @classmethod

@@ -1,0 +1,312 @@
+"""A local DC/OS stand-in that runs the SDK's frameworks end to end on one machine.
+
+Reference: the system-integration tier of the reference (``testing/sdk_*.py`` driving
+``frameworks/*/tests`` against a live DC/OS cluster). Pieces:
+
+* **ZooKeeper** -- ``testing.zk_server.ZkServer`` (jute wire protocol); schedulers persist to it
+  with ``SDK_PERSISTER=zk`` exactly as on DC/OS (``/dcos-service-<name>`` trees, service lock);
+* **Mesos master + agents** -- ``LocalMaster`` behind ``HttpMaster`` (Mesos v1 scheduler HTTP
+  API); agents carry hostnames, fault domains (region/zone), attributes and optional MI355X GPUs;
+  with ``executor="process"`` every task command really runs (``mesos.containerizer``), with
+  ``executor="synthetic"`` tasks follow a timeline (``finish_tasks`` names the ones that exit 0);
+* **Marathon** -- ``LocalMarathon`` runs every scheduler as a supervised OS process;
+* **Cosmos** -- ``LocalCosmos`` installs the universe packages under ``frameworks/*/universe``;
+* **DNS** -- names under the cluster TLDs (``*.thisdcos.directory``, ``*.mesos``) resolve to the
+  loopback address for the task fetcher;
+* **fault injection** -- agent partition/reconnect, agent shutdown, agent decommission (GONE),
+  ``pkill``-style kills inside task sessions, scheduler crashes.
+
+``current()`` is the cluster the ``testing.sdk`` helpers act on (``use(cluster)`` sets it).
+"""
+from __future__ import annotations
+
+import logging
+import os
+import shutil
+import tempfile
+import threading
+import time
+from dataclasses import dataclass, field
+from typing import Dict, Iterable, List, Optional, Sequence
+
+from dcos_commons_amd.mesos import protos as P
+from dcos_commons_amd.mesos.http_master import HttpMaster
+from dcos_commons_amd.mesos.local_master import TERMINAL, AgentSpec, LocalMaster, TaskBehavior, TaskTiming
+from dcos_commons_amd.testing.cluster.marathon import LocalMarathon
+from dcos_commons_amd.testing.cluster.packages import LocalCosmos
+from dcos_commons_amd.testing.zk_server import ZkServer
+
+LOGGER = logging.getLogger(__name__)
+CLUSTER_DNS_SUFFIXES = (".thisdcos.directory", ".mesos", ".dcos")
+DEFAULT_REGION = "us-west-2"
+DEFAULT_ZONES = ("us-west-2a", "us-west-2b", "us-west-2c")
+
+_current: Optional["LocalCluster"] = None
+_current_lock = threading.Lock()
+
+
+def current() -> "LocalCluster":
+    if _current is None:
+        raise RuntimeError("No local cluster is active: create one with LocalCluster(...).start() and use() it")
+    return _current
+
+
+def use(cluster: Optional["LocalCluster"]) -> None:
+    global _current
+    with _current_lock:
+        _current = cluster
+
+
+@dataclass
+class TaskView:
+    """One task as ``dcos task --json`` / ``/mesos/tasks`` show it."""
+    id: str
+    name: str
+    framework_id: str
+    framework_name: str
+    agent_id: str
+    host: str
+    state: str
+    resources: Dict[str, float]
+    labels: Dict[str, str]
+    statuses: List[P.TaskStatus] = field(default_factory=list)
+
+    @property
+    def is_terminal(self) -> bool:
+        return P.TaskState.Value(self.state) in TERMINAL
+
+
+class _SyntheticBehavior(TaskBehavior):
+    """Synthetic lifecycle; tasks whose name ends with one of ``finish_suffixes`` exit 0."""
+
+    def __init__(self, finish_suffixes: Sequence[str], finish_after_s: float = 0.2):
+        super().__init__(TaskTiming())
+        self.finish_suffixes = tuple(finish_suffixes)
+        self.finish = TaskTiming(finish_after_s=finish_after_s, exit_state=P.TASK_FINISHED)
+
+    def timing(self, task: P.TaskInfo) -> TaskTiming:
+        if self.finish_suffixes and task.name.endswith(self.finish_suffixes):
+            return self.finish
+        return self.default
+
+
+class LocalCluster:
+    def __init__(self, agents: int = 5, agent_specs: Optional[Iterable[AgentSpec]] = None,
+                 work_dir: Optional[str] = None, executor: str = "process", allocation_interval_s: float = 0.1,
+                 region: str = DEFAULT_REGION, zones: Sequence[str] = DEFAULT_ZONES, gpus_per_agent: int = 0,
+                 agent_cpus: float = 8.0, agent_mem: float = 32768.0, agent_disk: float = 65536.0,
+                 packages: Optional[Dict[str, str]] = None, scheduler_env: Optional[Dict[str, str]] = None,
+                 finish_tasks: Sequence[str] = (), dcos_version: str = "1.13.0", keep_work_dir: bool = False):
+        self.work_dir = os.path.abspath(work_dir or tempfile.mkdtemp(prefix="sdk-cluster-"))
+        self._own_work_dir = work_dir is None and not keep_work_dir
+        self.region = region
+        self.dcos_version = dcos_version
+        self.extra_scheduler_env = dict(scheduler_env or {})
+        self.secrets: Dict[str, bytes] = {}
+        if executor == "process":
+            from dcos_commons_amd.mesos.containerizer import ProcessTaskBehavior
+
+            self.behavior = ProcessTaskBehavior(os.path.join(self.work_dir, "agents"),
+                                                secret_resolver=self.secrets.get, resolver=self.resolve)
+        elif executor == "synthetic":
+            self.behavior = _SyntheticBehavior(finish_tasks)
+        else:
+            raise ValueError(f"executor must be 'process' or 'synthetic', not {executor!r}")
+        self.executor = executor
+        if agent_specs is None:
+            agent_specs = [AgentSpec(hostname=f"10.0.0.{i + 1}", cpus=agent_cpus, mem=agent_mem, disk=agent_disk,
+                                     region=region, zone=zones[i % len(zones)] if zones else None,
+                                     gpus=gpus_per_agent,
+                                     attributes=({"gpu_vendor": "amd", "gpu_model": "MI355X"}
+                                                 if gpus_per_agent else {}))
+                           for i in range(agents)]
+        self._agent_specs = list(agent_specs)
+        domain = P.DomainInfo()
+        domain.fault_domain.region.name = region
+        domain.fault_domain.zone.name = zones[0] if zones else "local"
+        self.master = LocalMaster(allocation_interval_s=allocation_interval_s, behavior=self.behavior, domain=domain)
+        self.master.add_status_listener(self._on_status)
+        self._tasks: Dict[str, TaskView] = {}
+        self._tasks_lock = threading.Lock()
+        self.agent_ids: Dict[str, str] = {}  # hostname -> agent id
+        self.zk: Optional[ZkServer] = None
+        self.http_master: Optional[HttpMaster] = None
+        self.marathon = LocalMarathon(self)
+        self.cosmos = LocalCosmos(self, packages)
+        self._started = False
+
+    # -- lifecycle -------------------------------------------------------------------------
+    def start(self) -> "LocalCluster":
+        self.zk = ZkServer().start()
+        self.http_master = HttpMaster(self.master).start()
+        for spec in self._agent_specs:
+            self.agent_ids[spec.hostname] = self.master.add_agent(spec)
+        self._started = True
+        return self
+
+    def shutdown(self) -> None:
+        if not self._started:
+            return
+        self._started = False
+        self.marathon.shutdown()
+        if self.http_master is not None:
+            self.http_master.stop()
+        self.master.shutdown()
+        if self.zk is not None:
+            self.zk.stop()
+        if _current is self:
+            use(None)
+        if self._own_work_dir:
+            shutil.rmtree(self.work_dir, ignore_errors=True)
+
+    def __enter__(self) -> "LocalCluster":
+        if not self._started:
+            self.start()
+        use(self)
+        return self
+
+    def __exit__(self, *exc) -> None:
+        self.shutdown()
+
+    # -- what Marathon hands every scheduler ---------------------------------------------------
+    def scheduler_environment(self) -> Dict[str, str]:
+        env = {
+            "SDK_MESOS_MASTER": self.http_master.url, "SDK_MESOS_CONTENT_TYPE": "protobuf",
+            "SDK_PERSISTER": "zk", "SDK_ZOOKEEPER": self.zk.connect_string,
+            "SDK_API_HOST": "127.0.0.1", "DCOS_VERSION": self.dcos_version,
+            "FRAMEWORK_LOG_LEVEL": "INFO",
+        }
+        env.update(self.extra_scheduler_env)
+        return env
+
+    @staticmethod
+    def resolve(hostname: str) -> Optional[str]:
+        if hostname in ("localhost", "127.0.0.1") or hostname.endswith(CLUSTER_DNS_SUFFIXES):
+            return "127.0.0.1"
+        return None
+
+    # -- master views -----------------------------------------------------------------------
+    def _on_status(self, framework_id: str, status: P.TaskStatus) -> None:
+        # runs on the master's actor thread: master state is consistent here
+        tid = status.task_id.value
+        with self._tasks_lock:
+            view = self._tasks.get(tid)
+            if view is None:
+                t = self.master._find_task(tid)
+                if t is None:
+                    return
+                fw = self.master.frameworks.get(framework_id)
+                agent = self.master.agents.get(t.agent_id)
+                res: Dict[str, float] = {}
+                for r in t.info.resources:
+                    if r.type == P.Value.SCALAR:
+                        res[r.name] = res.get(r.name, 0.0) + r.scalar.value
+                    elif r.type == P.Value.RANGES:
+                        res.setdefault(r.name, 0.0)
+                view = TaskView(tid, t.info.name, framework_id, fw.info.name if fw is not None else "",
+                                t.agent_id, agent.spec.hostname if agent is not None else "", "TASK_STAGING", res,
+                                {l.key: l.value for l in t.info.labels.labels})
+                self._tasks[tid] = view
+            view.state = P.TaskState.Name(status.state)
+            view.statuses.append(status)
+
+    def frameworks(self, include_inactive: bool = False) -> List[dict]:
+        def do():
+            return [{"id": fid, "name": fw.info.name, "active": fw.connected, "roles": sorted(fw.roles)}
+                    for fid, fw in self.master.frameworks.items() if include_inactive or fw.connected]
+        return self.master.call(do)
+
+    def framework_ids(self, name: str) -> List[str]:
+        return [f["id"] for f in self.frameworks(include_inactive=True) if f["name"] == name]
+
+    def tasks(self, framework_name: Optional[str] = None, include_terminal: bool = False) -> List[TaskView]:
+        with self._tasks_lock:
+            views = list(self._tasks.values())
+        out = []
+        for v in views:
+            if framework_name is not None and v.framework_name != framework_name:
+                continue
+            if not include_terminal and v.is_terminal:
+                continue
+            out.append(v)
+        return sorted(out, key=lambda v: (v.name, v.statuses[0].timestamp if v.statuses else 0.0))
+
+    def task(self, task_id: str) -> Optional[TaskView]:
+        with self._tasks_lock:
+            return self._tasks.get(task_id)
+
+    def agents(self) -> List[dict]:
+        def do():
+            out = []
+            for aid, a in self.master.agents.items():
+                out.append({"id": aid, "hostname": a.spec.hostname, "active": a.active, "zone": a.spec.zone,
+                            "region": a.spec.region, "attributes": dict(a.spec.attributes), "gpus": a.spec.gpus})
+            return out
+        return self.master.call(do)
+
+    def reserved_resources(self, role: Optional[str] = None) -> List[tuple]:
+        """(agent hostname, resource) for every dynamically reserved resource (optionally of one
+        role) still held on an agent -- what an uninstall must leave empty."""
+        from dcos_commons_amd.mesos.resource_math import effective_role
+
+        out = []
+        for a in self.agents():
+            for r in self.master.reserved_resources(a["id"]):
+                if role is None or effective_role(r) == role:
+                    out.append((a["hostname"], r))
+        return out
+
+    def zk_children(self, path: str = "/") -> List[str]:
+        from dcos_commons_amd.storage.zookeeper import ZkClient
+
+        c = ZkClient(self.zk.connect_string).start()
+        try:
+            return sorted(c.get_children(path))
+        finally:
+            c.close()
+
+    # -- fault injection ------------------------------------------------------------------
+    def _agent(self, host: str) -> str:
+        aid = self.agent_ids.get(host)
+        if aid is None:
+            raise KeyError(f"no agent with hostname {host}")
+        return aid
+
+    def partition_agent(self, host: str) -> None:
+        self.master.lose_agent(self._agent(host))
+
+    def reconnect_agent(self, host: str) -> None:
+        self.master.reconnect_agent(self._agent(host))
+
+    def decommission_agent(self, host: str) -> None:
+        """The operator marks the agent GONE (``dcos node decommission``)."""
+        self.master.gone_by_operator(self._agent(host))
+
+    def add_agent(self, spec: AgentSpec) -> str:
+        aid = self.master.add_agent(spec)
+        self.agent_ids[spec.hostname] = aid
+        return aid
+
+    def kill_task_with_pattern(self, pattern: str, agent_host: Optional[str] = None) -> int:
+        if self.executor != "process":
+            raise RuntimeError("pattern kills need the process executor")
+        return self.behavior.kill_with_pattern(pattern, agent_host)
+
+    def fail_task(self, task_id: str, state: int = P.TASK_FAILED) -> None:
+        """Synthetic-executor equivalent of killing a task's process."""
+        self.master.fail_task(task_id, state)
+
+    def task_exec(self, task_id: str, cmd: str, timeout_s: float = 30.0):
+        if self.executor != "process":
+            raise RuntimeError("task exec needs the process executor")
+        return self.behavior.exec_in_task(task_id, cmd, timeout_s)
+
+    def wait(self, predicate, timeout_s: float = 60.0, interval_s: float = 0.05, what: str = "condition"):
+        deadline = time.time() + timeout_s
+        while True:
+            v = predicate()
+            if v:
+                return v
+            if time.time() >= deadline:
+                raise TimeoutError(f"timed out after {timeout_s}s waiting for {what}")
+            time.sleep(interval_s)

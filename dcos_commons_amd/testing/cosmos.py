@@ -75,7 +75,10 @@ def option_defaults(universe_dir: str, build_params: Optional[Mapping[str, str]]
 
 
 def render_marathon_app(universe_dir: str, options: Optional[Mapping[str, str]] = None,
-                        build_params: Optional[Mapping[str, str]] = None) -> Dict:
+                        build_params: Optional[Mapping[str, str]] = None,
+                        package_params: Optional[Mapping[str, str]] = None) -> Dict:
+    """``package_params`` override the test package coordinates (``package-name``,
+    ``package-version``, ...) that otherwise default to ``MARATHON_TEMPLATE_PARAMS``."""
     build_params = dict(build_params or {})
     params = option_defaults(universe_dir, build_params)
     resource_path = os.path.join(universe_dir, "resource.json")
@@ -91,6 +94,7 @@ def render_marathon_app(universe_dir: str, options: Optional[Mapping[str, str]] 
     params.update({k: _scalar(v).replace('"', '\\"') for k, v in (options or {}).items()})
     params.update(build_params)
     params.update(MARATHON_TEMPLATE_PARAMS)
+    params.update(package_params or {})
     text = T.render_mustache_throw_if_missing("universe/marathon.json.mustache",
                                               _read(os.path.join(universe_dir, "marathon.json.mustache")), params)
     return json.loads(text)
