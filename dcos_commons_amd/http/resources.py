@@ -345,7 +345,7 @@ class PodResource:
         tasks = GroupedTasks(self.state_store).pod_instance_tasks(name)
         if tasks is None:
             return not_found(f"Pod {name}")
-        return json_ok([{"info": P.to_json(i), "status": P.to_json(s) if s is not None else None}
+        return json_ok([{"info": P.to_v0_json(i), "status": P.to_v0_json(s) if s is not None else None}
                         for i, s in tasks])
 
     def override(self, name: str, body: str, override: GoalStateOverride) -> Response:

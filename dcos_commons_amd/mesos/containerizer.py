@@ -86,6 +86,15 @@ def _session_pids(sid: int) -> List[int]:
     return out
 
 
+def _start_ticks(pid: int) -> int:
+    try:
+        with open(f"/proc/{pid}/stat", "rb") as f:
+            stat = f.read().decode("utf-8", "replace")
+        return int(stat[stat.rindex(")") + 2:].split()[19])
+    except (OSError, ValueError, IndexError):
+        return 1 << 62
+
+
 def _cmdline(pid: int) -> str:
     try:
         with open(f"/proc/{pid}/cmdline", "rb") as f:
@@ -381,24 +390,31 @@ class ProcessTaskBehavior(TaskBehavior):
                            capture_output=True, timeout=timeout_s, start_new_session=True)
         return r.returncode, r.stdout.decode("utf-8", "replace"), r.stderr.decode("utf-8", "replace")
 
-    def kill_with_pattern(self, pattern: str, agent_host: Optional[str] = None, sig: int = signal.SIGKILL) -> int:
-        """``pkill -<sig> -f <pattern>`` over the processes of the tasks this runtime started
-        (optionally only on one agent). Returns how many processes were signalled."""
+    def kill_with_pattern(self, pattern: str, agent_host: Optional[str] = None, sig: int = signal.SIGKILL,
+                          oldest: bool = False) -> int:
+        """``pkill [-o] -<sig> -f <pattern>`` over the processes of the tasks this runtime started
+        (optionally only on one agent; ``oldest``: only the longest-running match). Returns how
+        many processes were signalled."""
         rx = re.compile(pattern)
         with self._lock:
             procs = [p for p in self._procs.values() if not p.exited.is_set()
                      and (agent_host is None or p.agent_host == agent_host)]
-        n = 0
+        matches = []
         for p in procs:
             if p.popen is None:
                 continue
             for pid in _session_pids(p.popen.pid):
                 if rx.search(_cmdline(pid)):
-                    try:
-                        os.kill(pid, sig)
-                        n += 1
-                    except ProcessLookupError:
-                        pass
+                    matches.append(pid)
+        if oldest and matches:
+            matches = [min(matches, key=_start_ticks)]
+        n = 0
+        for pid in matches:
+            try:
+                os.kill(pid, sig)
+                n += 1
+            except ProcessLookupError:
+                pass
         return n
 
     def running_task_ids(self) -> List[str]:

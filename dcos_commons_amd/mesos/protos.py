@@ -256,3 +256,22 @@ def from_json(cls, data):
 
 def to_text(msg) -> str:
     return text_format.MessageToString(msg, as_one_line=True)
+
+
+_V0_NAMES = {"agentId": "slaveId", "agentInfo": "slaveInfo"}
+
+
+def _rename_v0(node):
+    if isinstance(node, dict):
+        return {_V0_NAMES.get(k, k): _rename_v0(v) for k, v in node.items()}
+    if isinstance(node, list):
+        return [_rename_v0(v) for v in node]
+    return node
+
+
+def to_v0_json(msg) -> dict:
+    """JSON as the reference's HTTP API renders Mesos protos (Jackson protobuf module over the v0
+    ``org.apache.mesos.Protos``): camelCase field names and the v0 ``slave*`` names, e.g.
+    ``{"taskId": {...}, "slaveId": {...}}`` (helloworld/tests/test_sanity.py:231)."""
+    return _rename_v0(json_format.MessageToDict(msg))
+

@@ -287,10 +287,10 @@ class LocalCluster:
         self.agent_ids[spec.hostname] = aid
         return aid
 
-    def kill_task_with_pattern(self, pattern: str, agent_host: Optional[str] = None) -> int:
+    def kill_task_with_pattern(self, pattern: str, agent_host: Optional[str] = None, oldest: bool = False) -> int:
         if self.executor != "process":
             raise RuntimeError("pattern kills need the process executor")
-        return self.behavior.kill_with_pattern(pattern, agent_host)
+        return self.behavior.kill_with_pattern(pattern, agent_host, oldest=oldest)
 
     def fail_task(self, task_id: str, state: int = P.TASK_FAILED) -> None:
         """Synthetic-executor equivalent of killing a task's process."""

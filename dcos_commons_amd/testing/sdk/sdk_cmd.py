@@ -1,0 +1,337 @@
+"""Requests and commands against services on the local cluster.
+
+Reference: testing/sdk_cmd.py. What goes where here:
+
+* ``service_request`` -- HTTP to the scheduler's API (what the adminrouter path
+  ``/service/<name>/...`` reaches on DC/OS);
+* ``cluster_request`` -- cluster-level endpoints of the stand-in (``/mesos/state-summary``,
+  ``/mesos/frameworks``, ``/marathon/v2/apps/<id>``, ``/dcos-metadata/dcos-version.json``);
+* ``svc_cli`` -- the service CLI (``native/build/sdk-cli``) pointed at the service; ``describe``
+  and ``update start`` go to Cosmos, as the DC/OS CLI does;
+* ``run_cli`` -- the subset of ``dcos`` commands the tests use (``package install|uninstall``,
+  ``<package> --name=<svc> <cmd>``, ``task exec``);
+* ``kill_task_with_pattern`` / ``service_task_exec`` -- ``pkill`` and ``dcos task exec`` inside
+  task sandboxes (real processes, see ``mesos.containerizer``).
+"""
+from __future__ import annotations
+
+import json
+import logging
+import os
+import shlex
+import subprocess
+import time
+import urllib.error
+import urllib.request
+from typing import Any, Dict, List, Optional, Tuple
+
+LOG = logging.getLogger(__name__)
+REPO_ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+CLI_BINARY = os.path.join(REPO_ROOT, "native", "build", "sdk-cli")
+
+
+def _cluster():
+    from dcos_commons_amd.testing.cluster import current
+
+    return current()
+
+
+class Response:
+    """The parts of ``requests.Response`` the tests use."""
+
+    def __init__(self, status_code: int, content: bytes, headers: Optional[Dict[str, str]] = None, url: str = ""):
+        self.status_code = status_code
+        self.content = content
+        self.headers = dict(headers or {})
+        self.url = url
+
+    @property
+    def ok(self) -> bool:
+        return 200 <= self.status_code < 400
+
+    @property
+    def text(self) -> str:
+        return self.content.decode("utf-8", "replace")
+
+    def json(self) -> Any:
+        return json.loads(self.content.decode("utf-8") or "null")
+
+    def raise_for_status(self) -> None:
+        if not self.ok:
+            raise HTTPError(self)
+
+    def __repr__(self) -> str:
+        return f"<Response [{self.status_code}] {self.url}>"
+
+
+class HTTPError(Exception):
+    def __init__(self, response: Response):
+        super().__init__(f"HTTP {response.status_code} for {response.url}: {response.text[:500]}")
+        self.response = response
+
+
+def _http(method: str, url: str, data: Optional[bytes], headers: Dict[str, str], timeout_s: float) -> Response:
+    req = urllib.request.Request(url, data=data, method=method.upper(), headers=headers)
+    try:
+        with urllib.request.urlopen(req, timeout=timeout_s) as r:
+            return Response(r.status, r.read(), dict(r.headers), url)
+    except urllib.error.HTTPError as e:
+        return Response(e.code, e.read() or b"", dict(e.headers or {}), url)
+
+
+def _body(kwargs: Dict[str, Any]) -> Tuple[Optional[bytes], Dict[str, str]]:
+    headers = dict(kwargs.get("headers") or {})
+    if "json" in kwargs and kwargs["json"] is not None:
+        headers.setdefault("Content-Type", "application/json")
+        return json.dumps(kwargs["json"]).encode("utf-8"), headers
+    data = kwargs.get("data")
+    if isinstance(data, str):
+        data = data.encode("utf-8")
+    return data, headers
+
+
+def service_request(method: str, service_name: str, service_path: str, retry: bool = True,
+                    raise_on_error: bool = True, log_args: bool = True, log_response: bool = False,
+                    timeout_seconds: int = 60, **kwargs: Any) -> Response:
+    """``method`` ``service_path`` on the service's scheduler API, e.g.
+    ``service_request("GET", "/test/integration/hello-world", "/v1/plans/deploy")``."""
+    path = "/" + service_path.lstrip("/")
+    data, headers = _body(kwargs)
+    deadline = time.time() + timeout_seconds
+    while True:
+        try:
+            base = _cluster().marathon.scheduler_url(service_name)
+            if log_args:
+                LOG.info("(SDK) %s %s%s", method, service_name, path)
+            resp = _http(method, base + path, data, headers, max(1.0, deadline - time.time()))
+            if log_response:
+                LOG.info("(SDK) -> %s %s", resp.status_code, resp.text[:1000])
+            if raise_on_error and not resp.ok and resp.status_code not in (202, 208):
+                raise HTTPError(resp)
+            return resp
+        except (HTTPError, urllib.error.URLError, OSError, KeyError) as e:
+            if not retry or time.time() >= deadline:
+                if isinstance(e, HTTPError) or raise_on_error:
+                    raise
+                return Response(0, str(e).encode(), {}, path)
+            time.sleep(0.2)
+
+
+def _state_summary() -> dict:
+    c = _cluster()
+    by_agent: Dict[str, Dict[str, List[dict]]] = {}
+    for host, r in c.reserved_resources():
+        from dcos_commons_amd.mesos.resource_math import effective_role
+
+        by_agent.setdefault(host, {}).setdefault(effective_role(r), []).append(
+            {"name": r.name, "scalar": r.scalar.value if r.HasField("scalar") else None})
+    slaves = [{"id": a["id"], "hostname": a["hostname"], "active": a["active"],
+               "reserved_resources": by_agent.get(a["hostname"], {}),
+               "domain": {"fault_domain": {"region": {"name": a["region"]}, "zone": {"name": a["zone"]}}},
+               "attributes": a["attributes"]} for a in c.agents()]
+    frameworks = [{"id": f["id"], "name": f["name"], "active": f["active"], "roles": f["roles"]}
+                  for f in c.frameworks()]
+    return {"slaves": slaves, "frameworks": frameworks}
+
+
+def cluster_request(method: str, cluster_path: str, retry: bool = True, raise_on_error: bool = True,
+                    log_args: bool = True, log_response: bool = False, timeout_seconds: int = 60,
+                    **kwargs: Any) -> Response:
+    """Cluster-level endpoints of the local DC/OS stand-in."""
+    c = _cluster()
+    path = "/" + cluster_path.lstrip("/")
+    if log_args:
+        LOG.info("(SDK) %s %s", method, path)
+    m = method.upper()
+    body: Any = None
+    status = 200
+    try:
+        if path in ("/mesos/state-summary", "/mesos/master/state-summary", "/mesos/state", "/mesos/master/state"):
+            body = _state_summary()
+        elif path in ("/mesos/frameworks", "/mesos/master/frameworks"):
+            body = {"frameworks": c.frameworks(include_inactive=True)}
+        elif path in ("/mesos/tasks", "/mesos/master/tasks"):
+            body = {"tasks": [{"id": t.id, "name": t.name, "state": t.state, "framework_id": t.framework_id,
+                               "slave_id": t.agent_id} for t in c.tasks(include_terminal=True)]}
+        elif path == "/dcos-metadata/dcos-version.json":
+            body = {"version": c.dcos_version, "dcos-variant": "open"}
+        elif path.startswith("/marathon/v2/apps"):
+            app_id = path[len("/marathon/v2/apps"):].split("?")[0]
+            if m == "GET" and not app_id.strip("/"):
+                body = {"apps": [c.marathon.get_app(a) for a in c.marathon.app_ids()]}
+            elif m == "GET":
+                body = {"app": c.marathon.get_app(app_id)}
+            elif m == "PUT":
+                data, _ = _body(kwargs)
+                c.marathon.update_app(json.loads(data), wait=False)
+                body = {"deploymentId": "local"}
+            elif m == "DELETE":
+                c.marathon.destroy_app(app_id)
+                body = {"deploymentId": "local"}
+            elif m == "POST" and app_id.endswith("/restart"):
+                c.marathon.restart_app(app_id[: -len("/restart")], wait=False)
+                body = {"deploymentId": "local"}
+            elif m == "POST":
+                data, _ = _body(kwargs)
+                body = c.marathon.install_app(json.loads(data), wait=False)
+                status = 201
+        else:
+            status, body = 404, {"message": f"no such endpoint in the local cluster: {path}"}
+    except KeyError as e:
+        status, body = 404, {"message": str(e)}
+    resp = Response(status, json.dumps(body).encode("utf-8"), {"Content-Type": "application/json"}, path)
+    if log_response:
+        LOG.info("(SDK) -> %s %s", status, resp.text[:1000])
+    if raise_on_error and not resp.ok:
+        raise HTTPError(resp)
+    return resp
+
+
+# -- CLI ----------------------------------------------------------------------------------------
+def _run(argv: List[str], print_output: bool, check: bool, timeout_seconds: Optional[int] = 120,
+         env: Optional[Dict[str, str]] = None) -> Tuple[int, str, str]:
+    r = subprocess.run(argv, capture_output=True, timeout=timeout_seconds, env=env)
+    out, err = r.stdout.decode("utf-8", "replace"), r.stderr.decode("utf-8", "replace")
+    if print_output:
+        LOG.info("(SDK) %s -> rc=%d\n%s%s", " ".join(argv), r.returncode, out, err)
+    if check and r.returncode != 0:
+        raise subprocess.CalledProcessError(r.returncode, argv, out, err)
+    return r.returncode, out, err
+
+
+def _cosmos_cli(service_name: str, args: List[str]) -> Tuple[int, str, str]:
+    """``dcos <pkg> describe`` / ``update start`` are Cosmos calls in the DC/OS CLI too."""
+    c = _cluster()
+    if args[0] == "describe":
+        return 0, json.dumps(c.cosmos.describe(service_name), indent=2) + "\n", ""
+    options: Dict[str, Any] = {}
+    version = None
+    replace = False
+    for a in args[2:]:
+        if a.startswith("--options="):
+            with open(a.split("=", 1)[1], "r", encoding="utf-8") as f:
+                options = json.load(f)
+        elif a.startswith("--package-version="):
+            version = a.split("=", 1)[1]
+        elif a == "--replace":
+            replace = True
+    try:
+        c.cosmos.update(service_name, options, version=version, replace=replace, wait=True)
+    except (KeyError, ValueError) as e:
+        return 1, "", f"{e}\n"
+    return 0, "Update started. Please use `dcos {} update status` to view progress.\n".format(
+        service_name.strip("/")), ""
+
+
+def svc_cli(package_name: str, service_name: str, service_cmd: str, print_output: bool = True,
+            parse_json: bool = False, check: bool = False) -> Tuple[int, Any, str]:
+    """``dcos <package> --name=<service> <service_cmd>``; ``parse_json`` decodes stdout."""
+    args = shlex.split(service_cmd)
+    if args and (args[0] == "describe" or args[:2] == ["update", "start"]):
+        rc, out, err = _cosmos_cli(service_name, args)
+    else:
+        flags = [a for a in args if a == "--json"]
+        rest = [a for a in args if a != "--json"]
+        url = _cluster().marathon.scheduler_url(service_name)
+        rc, out, err = _run([CLI_BINARY, "--url", url] + flags + rest, print_output, False)
+    if check and rc != 0:
+        raise subprocess.CalledProcessError(rc, service_cmd, out, err)
+    if parse_json and rc == 0:
+        return rc, json.loads(out or "null"), err
+    return rc, out, err
+
+
+def run_cli(cmd: str, print_output: bool = True, check: bool = False) -> Tuple[int, str, str]:
+    """The ``dcos`` CLI commands the tests use."""
+    args = shlex.split(cmd)
+    c = _cluster()
+    rc, out, err = 1, "", f"unsupported command in the local cluster: dcos {cmd}\n"
+    if args[:2] == ["package", "install"]:
+        opts: Dict[str, Any] = {}
+        name, version = args[2], None
+        app_id = None
+        for a in args[3:]:
+            if a.startswith("--options="):
+                with open(a.split("=", 1)[1], "r", encoding="utf-8") as f:
+                    opts = json.load(f)
+            elif a.startswith("--package-version="):
+                version = a.split("=", 1)[1]
+            elif a.startswith("--app-id="):
+                app_id = a.split("=", 1)[1]
+        c.cosmos.install(name, app_id, opts, version=version, wait=True)
+        rc, out, err = 0, f"Installing package [{name}]\n", ""
+    elif args[:2] == ["package", "uninstall"]:
+        app_id = next((a.split("=", 1)[1] for a in args if a.startswith("--app-id=")), args[2])
+        c.cosmos.uninstall(app_id)
+        rc, out, err = 0, f"Uninstalled package [{args[2]}]\n", ""
+    elif args[:2] == ["task", "exec"]:
+        rc, out, err = service_task_exec(None, args[2], " ".join(args[3:]))
+    elif len(args) >= 2 and args[1].startswith("--name="):
+        return svc_cli(args[0], args[1].split("=", 1)[1], " ".join(shlex.quote(a) for a in args[2:]),
+                       print_output, False, check)
+    if print_output:
+        LOG.info("(SDK) dcos %s -> rc=%d\n%s%s", cmd, rc, out, err)
+    if check and rc != 0:
+        raise subprocess.CalledProcessError(rc, cmd, out, err)
+    return rc, out, err
+
+
+# -- tasks --------------------------------------------------------------------------------------
+def kill_task_with_pattern(pattern: str, user: str = "nobody", agent_host: Optional[str] = None) -> bool:
+    """``pkill -9 -o -f <pattern>`` inside the task sandboxes (of one agent): the oldest matching
+    process dies. Returns whether anything was killed."""
+    return _cluster().kill_task_with_pattern(pattern, agent_host, oldest=True) > 0
+
+
+def _find_task_id(service_name: Optional[str], task_name: str) -> str:
+    from dcos_commons_amd.testing.sdk import sdk_tasks
+
+    tasks = [t for t in sdk_tasks.get_service_tasks(service_name or "", task_prefix=task_name)
+             if t.name == task_name or t.id == task_name] if service_name else \
+        [t for t in _cluster().tasks() if t.name == task_name or t.id == task_name]
+    if not tasks:
+        raise KeyError(f"no running task named {task_name}")
+    return tasks[-1].id
+
+
+def service_task_exec(service_name: Optional[str], task_name: str, cmd: str) -> Tuple[int, str, str]:
+    """``dcos task exec <task> <cmd>``: runs in the task's sandbox with its environment."""
+    tid = _find_task_id(service_name, task_name)
+    return _cluster().task_exec(tid, cmd)
+
+
+def marathon_task_exec(task_name: str, cmd: str, print_output: bool = True) -> Tuple[int, str, str]:
+    """Runs ``cmd`` in the sandbox of the scheduler (Marathon task) named ``task_name``."""
+    c = _cluster()
+    for app_id in c.marathon.app_ids():
+        sandbox = c.marathon.sandbox(app_id)
+        from dcos_commons_amd.testing.cluster import scheduler_task_prefix
+
+        if scheduler_task_prefix(app_id).startswith(task_name) or app_id.strip("/") == task_name.strip("/"):
+            return _run(["bash", "-c", cmd], print_output, False, env=None) if sandbox is None else \
+                _run(["bash", "-c", f"cd {shlex.quote(sandbox)} && {cmd}"], print_output, False)
+    return 1, "", f"no marathon task {task_name}\n"
+
+
+def get_task_sandbox_path(task_id: str) -> str:
+    c = _cluster()
+    path = c.behavior.sandbox_of(task_id) if c.executor == "process" else None
+    if path is None:
+        raise KeyError(task_id)
+    return path
+
+
+def create_task_text_file(marathon_task_name: str, filename: str, lines: List[str]) -> bool:
+    rc, _, _ = marathon_task_exec(marathon_task_name, "cat > {} <<'EOF'\n{}\nEOF".format(
+        shlex.quote(filename), "\n".join(lines)))
+    return rc == 0
+
+
+def resolve_hosts(marathon_task_name: str, hosts: List[str], bootstrap_cmd: str = "./bootstrap") -> bool:
+    """Every cluster DNS name resolves on the stand-in (to the loopback address)."""
+    return all(_cluster().resolve(h) is not None for h in hosts)
+
+
+def get_bash_command(cmd: str, environment: Optional[str]) -> str:
+    env_str = f"{environment} && " if environment else ""
+    return f'bash -c "{env_str}{cmd}"'

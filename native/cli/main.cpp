@@ -138,7 +138,9 @@ void usage() {
       "  debug config list|show ID|target|target_id\n"
       "  debug state framework_id|properties|property NAME|refresh_cache\n"
       "  debug pod pause|resume POD [-t TASK]...\n"
-      "  describe | update status | health | metrics\n"
+      "  describe | update status|force-complete|force-restart|pause|resume [PHASE [STEP]] | health | metrics\n"
+      "  aliases: plans, pods, endpoint; plan show|interrupt|continue|restart|force; debug configs|pods;\n"
+      "           deprecated top-level `config ...` and `state ...` (= debug config / debug state)\n"
       "  hdfs <hdfs args...>   (hdfs services: runs bin/hdfs on name-0-node via `dcos task exec`)\n";
 }
 
@@ -222,8 +224,18 @@ int plan_command(Ctx& c, const std::string& path, const std::string& target, con
   return 0;
 }
 
+// Reference command aliases (cli/commands/plan.go:61-85): show, interrupt, continue, restart, force.
+std::string plan_alias(const std::string& cmd) {
+  if (cmd == "show") return "status";
+  if (cmd == "interrupt") return "pause";
+  if (cmd == "continue") return "resume";
+  if (cmd == "restart") return "force-restart";
+  if (cmd == "force") return "force-complete";
+  return cmd;
+}
+
 int plan_cmd(Ctx& c, const std::vector<std::string>& a) {
-  std::string cmd = arg(a, 0);
+  std::string cmd = plan_alias(arg(a, 0));
   if (cmd == "list") return emit(call(c, "GET", "/plans"));
   if (cmd == "status") {
     std::string plan = arg(a, 1, "deploy");
@@ -310,6 +322,8 @@ int pod_cmd(Ctx& c, const std::vector<std::string>& a) {
 
 int debug_cmd(Ctx& c, const std::vector<std::string>& a) {
   std::string sec = arg(a, 0), cmd = arg(a, 1);
+  if (sec == "configs") sec = "config";
+  if (sec == "pods") sec = "pod";
   if (sec == "config") {
     if (cmd == "list") return emit(call(c, "GET", "/configurations"));
     if (cmd == "show") return emit(call(c, "GET", "/configurations/" + sdk::url_encode(arg(a, 2))));
@@ -374,6 +388,17 @@ int main(int argc, char** argv) {
   }
   std::string section = a[0];
   std::vector<std::string> rest(a.begin() + 1, a.end());
+  if (section == "plans") section = "plan";
+  if (section == "pods") section = "pod";
+  if (section == "endpoint") section = "endpoints";
+  if (section == "help") {
+    usage();
+    return 0;
+  }
+  if (section == "config" || section == "state") {  // deprecated top-level forms
+    rest.insert(rest.begin(), section);
+    section = "debug";
+  }
   try {
     if (section == "plan") return plan_cmd(c, rest);
     if (section == "pod") return pod_cmd(c, rest);
@@ -381,8 +406,10 @@ int main(int argc, char** argv) {
       return emit(call(c, "GET", rest.empty() ? "/endpoints" : "/endpoints/" + sdk::url_encode(rest[0])));
     if (section == "debug") return debug_cmd(c, rest);
     if (section == "describe") return emit(call(c, "GET", "/configurations/target"));
-    if (section == "update" && arg(rest, 0) == "status") {
-      std::vector<std::string> r2 = {"status", "deploy"};
+    if (section == "update" && !rest.empty() && rest[0] != "start" && rest[0] != "package-versions") {
+      // update <cmd> [PHASE [STEP]] acts on the deploy plan, which is the update plan once deployed
+      std::vector<std::string> r2 = {rest[0], "deploy"};
+      r2.insert(r2.end(), rest.begin() + 1, rest.end());
       return plan_cmd(c, r2);
     }
     if (section == "health") return emit(call(c, "GET", "/health?verbose=true"));

@@ -13,6 +13,7 @@ REFERENCE = "/root/reference"
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs on the GPU box)")
     config.addinivalue_line("markers", "slow: long-running")
+    config.addinivalue_line("markers", "integration: runs services on the local DC/OS stand-in")
 
 
 @pytest.fixture(autouse=True)
