@@ -47,6 +47,7 @@ from dcos_commons_amd.mesos.local_master import TaskBehavior, TaskTiming
 LOGGER = logging.getLogger(__name__)
 _LOOPBACK = {"127.0.0.1", "localhost", "::1"}
 DEFAULT_KILL_GRACE_S = 3.0
+EXECUTOR_ARGV0 = "mesos-default-executor"
 
 
 @dataclass
@@ -108,14 +109,18 @@ class ProcessTaskBehavior(TaskBehavior):
 
     def __init__(self, work_dir: str, secret_resolver: Optional[Callable[[str], Optional[bytes]]] = None,
                  default_kill_grace_s: float = DEFAULT_KILL_GRACE_S, extra_env: Optional[Dict[str, str]] = None,
-                 check_workers: int = 8, resolver: Optional[Callable[[str], Optional[str]]] = None):
+                 check_workers: int = 8, resolver: Optional[Callable[[str], Optional[str]]] = None,
+                 artifact_resolver: Optional[Callable[[str], Optional[str]]] = None):
         """``resolver(hostname)`` maps cluster DNS names to an address the fetcher can reach
-        (``None``: not a cluster name)."""
+        (``None``: not a cluster name); ``artifact_resolver(uri)`` maps a URI to a local file, or
+        to a directory whose contents stand for the extracted archive (e.g. ``bootstrap.zip`` ->
+        the native ``sdk-bootstrap`` as ``./bootstrap``)."""
         super().__init__(default=TaskTiming(), check_runner=self._run_readiness_check, check_workers=check_workers)
         self.work_dir = os.path.abspath(work_dir)
         os.makedirs(self.work_dir, exist_ok=True)
         self.secret_resolver = secret_resolver
         self.resolver = resolver
+        self.artifact_resolver = artifact_resolver
         self.default_kill_grace_s = default_kill_grace_s
         self.extra_env = dict(extra_env or {})
         self._procs: Dict[str, _Proc] = {}
@@ -153,8 +158,13 @@ class ProcessTaskBehavior(TaskBehavior):
             self._fetch(sandbox, info.command.uris)
             proc.env = self._environment(master, task, agent, sandbox)
             with open(os.path.join(sandbox, "stdout"), "ab") as out, open(os.path.join(sandbox, "stderr"), "ab") as err:
-                proc.popen = subprocess.Popen(["bash", "-c", info.command.value or "true"], cwd=sandbox,
-                                              env=proc.env, stdin=subprocess.DEVNULL, stdout=out, stderr=err,
+                # the task's shell is named like the executor that would run it on Mesos, so a
+                # `pkill -f mesos-default-executor` takes the task down with "its executor"
+                # (the trailing `exit $?` keeps that shell alive as the command's parent: bash
+                # would otherwise exec the last command of the list in its place)
+                proc.popen = subprocess.Popen([EXECUTOR_ARGV0, "-c", (info.command.value or "true") + "\nexit $?"],
+                                              executable="/bin/bash", cwd=sandbox, env=proc.env,
+                                              stdin=subprocess.DEVNULL, stdout=out, stderr=err,
                                               start_new_session=True)
         except Exception as e:  # noqa: BLE001
             LOGGER.exception("failed to start %s", info.name)
@@ -221,8 +231,19 @@ class ProcessTaskBehavior(TaskBehavior):
             dest = os.path.join(sandbox, name)
             addr = parsed.hostname if parsed.hostname in _LOOPBACK else (
                 self.resolver(parsed.hostname) if self.resolver is not None and parsed.hostname else None)
+            local = self.artifact_resolver(u.value) if self.artifact_resolver is not None else None
             try:
-                if parsed.scheme in ("", "file"):
+                if local is not None and os.path.isdir(local):
+                    for entry in os.listdir(local):   # the archive's extracted contents
+                        src = os.path.join(local, entry)
+                        if os.path.isdir(src):
+                            shutil.copytree(src, os.path.join(sandbox, entry), dirs_exist_ok=True)
+                        else:
+                            shutil.copy2(src, os.path.join(sandbox, entry))
+                    continue
+                if local is not None:
+                    shutil.copy2(local, dest)
+                elif parsed.scheme in ("", "file"):
                     shutil.copyfile(parsed.path, dest)
                 elif parsed.scheme in ("http", "https") and addr is not None:
                     url = u.value.replace(parsed.hostname, addr, 1)

@@ -11,7 +11,8 @@ Backends here (``SDK_PERSISTER``):
   (``storage.zk_persister``), optional digest credentials ``SDK_ZK_USERNAME``/``SDK_ZK_PASSWORD``.
   ``SDK_ZOOKEEPER`` replaces the connect string where the spec's default (``master.mesos:2181``)
   does not resolve, e.g. the local cluster of ``dcos_commons_amd.testing.cluster``.
-  ``SDK_LOCK_WAIT_S`` (default 10) is how long each of the 3 attempts waits for the service lock.
+  ``SDK_LOCK_WAIT_S`` (default 10) is how long each of the 3 attempts waits for the service lock;
+  ``SDK_ZK_SESSION_TIMEOUT_MS`` (default 10000) bounds how long a crashed scheduler's lock outlives it.
 
 Like ``CuratorPersister.Builder.build`` (:480-520) the durable backends first take the
 single-scheduler lock (``ZkLocker`` / ``FileLocker``; ``SDK_DISABLE_LOCK=true`` skips it, for tests)
@@ -105,10 +106,12 @@ def persister_for_service(service_spec, scheduler_config) -> Persister:
         connect = (env.get_optional("SDK_ZOOKEEPER", "") or service_spec.zookeeper_connection
                    or "127.0.0.1:2181")
         user, pw = env.get_optional("SDK_ZK_USERNAME", ""), env.get_optional("SDK_ZK_PASSWORD", "")
+        session_ms = env.get_optional_int("SDK_ZK_SESSION_TIMEOUT_MS", 10000)
         if lock_enabled and ZkLocker._instance is None:
             ZkLocker.lock(service_spec.name, connect, username=user, password=pw,
-                          wait_s=env.get_optional_double("SDK_LOCK_WAIT_S", 10.0))
-        base = ZooKeeperPersister(connect, service_spec.name, username=user, password=pw)
+                          wait_s=env.get_optional_double("SDK_LOCK_WAIT_S", 10.0), session_timeout_ms=session_ms)
+        base = ZooKeeperPersister(connect, service_spec.name, username=user, password=pw,
+                                  session_timeout_ms=session_ms)
         init_service_name(base, service_spec.name)
     else:
         raise ValueError(f"Unknown SDK_PERSISTER '{kind}' (expected file, mem or zk)")

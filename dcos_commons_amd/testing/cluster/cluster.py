@@ -102,12 +102,15 @@ class LocalCluster:
         self.region = region
         self.dcos_version = dcos_version
         self.extra_scheduler_env = dict(scheduler_env or {})
+        self.artifacts: Dict[str, str] = {}   # URI basename -> local file or extracted-archive directory
+        self._stage_native_artifacts()
         self.secrets: Dict[str, bytes] = {}
         if executor == "process":
             from dcos_commons_amd.mesos.containerizer import ProcessTaskBehavior
 
             self.behavior = ProcessTaskBehavior(os.path.join(self.work_dir, "agents"),
-                                                secret_resolver=self.secrets.get, resolver=self.resolve)
+                                                secret_resolver=self.secrets.get, resolver=self.resolve,
+                                                artifact_resolver=self.resolve_artifact)
         elif executor == "synthetic":
             self.behavior = _SyntheticBehavior(finish_tasks)
         else:
@@ -174,10 +177,33 @@ class LocalCluster:
             "SDK_MESOS_MASTER": self.http_master.url, "SDK_MESOS_CONTENT_TYPE": "protobuf",
             "SDK_PERSISTER": "zk", "SDK_ZOOKEEPER": self.zk.connect_string,
             "SDK_API_HOST": "127.0.0.1", "DCOS_VERSION": self.dcos_version,
+            # a killed scheduler's ZooKeeper lease (and lock) expires within 2 s, not 10
+            "SDK_ZK_SESSION_TIMEOUT_MS": "2000",
             "FRAMEWORK_LOG_LEVEL": "INFO",
         }
         env.update(self.extra_scheduler_env)
         return env
+
+    def _stage_native_artifacts(self) -> None:
+        """``bootstrap.zip`` (every SDK task fetches it) holds this tree's native ``sdk-bootstrap``."""
+        from dcos_commons_amd.testing.cluster.marathon import REPO_ROOT
+
+        binary = os.path.join(REPO_ROOT, "native", "build", "sdk-bootstrap")
+        if os.path.exists(binary):
+            d = os.path.join(self.work_dir, "artifacts", "bootstrap")
+            os.makedirs(d, exist_ok=True)
+            shutil.copy2(binary, os.path.join(d, "bootstrap"))
+            self.artifacts["bootstrap.zip"] = d
+
+    def register_artifact(self, basename: str, path: str) -> None:
+        """Tasks fetching a URI that ends in ``basename`` get ``path`` (a file, or a directory
+        standing for the extracted archive)."""
+        self.artifacts[basename] = path
+
+    def resolve_artifact(self, uri: str) -> Optional[str]:
+        import urllib.parse
+
+        return self.artifacts.get(os.path.basename(urllib.parse.urlparse(uri).path))
 
     @staticmethod
     def resolve(hostname: str) -> Optional[str]:
@@ -288,9 +314,31 @@ class LocalCluster:
         return aid
 
     def kill_task_with_pattern(self, pattern: str, agent_host: Optional[str] = None, oldest: bool = False) -> int:
-        if self.executor != "process":
-            raise RuntimeError("pattern kills need the process executor")
-        return self.behavior.kill_with_pattern(pattern, agent_host, oldest=oldest)
+        """``pkill -9 [-o] -f pattern`` on one host (or the master host when ``agent_host`` is None):
+        the processes of task sandboxes and of the scheduler processes Marathon runs (those run on
+        the loopback host). The cluster's own master and ZooKeeper are in-process: a pattern naming
+        them (``mesos-master``, ``QuorumPeerMain``) drops all their connections instead, which is
+        what their clients observe when the process dies and is restarted."""
+        import re as _re
+
+        if agent_host is None and _re.search(pattern, "mesos-master"):
+            self.http_master.drop_streams()
+            return 1
+        if agent_host is None and _re.search(pattern, "org.apache.zookeeper.server.quorum.QuorumPeerMain"):
+            self.zk.drop_connections()
+            return 1
+        n = 0
+        if agent_host in (None, "127.0.0.1", "localhost"):
+            n += self.marathon.kill_with_pattern(pattern, oldest=oldest)
+            if n and oldest:
+                return n
+        if self.executor == "process" and agent_host not in ("127.0.0.1", "localhost"):
+            n += self.behavior.kill_with_pattern(pattern, agent_host, oldest=oldest)
+        return n
+
+    def restart_master(self) -> None:
+        """Master failover as the schedulers see it: every event stream is cut."""
+        self.http_master.drop_streams()
 
     def fail_task(self, task_id: str, state: int = P.TASK_FAILED) -> None:
         """Synthetic-executor equivalent of killing a task's process."""

@@ -192,6 +192,27 @@ class LocalMarathon:
         os.killpg(proc.pid, sig)
         return task.id
 
+    def kill_with_pattern(self, pattern: str, oldest: bool = False) -> int:
+        """``pkill -9 -f`` over the scheduler processes (and their children)."""
+        import re
+
+        from dcos_commons_amd.mesos.containerizer import _cmdline, _session_pids, _start_ticks
+
+        rx = re.compile(pattern)
+        with self._lock:
+            procs = [a.proc for a in self._apps.values() if a.proc is not None and a.proc.poll() is None]
+        matches = [pid for p in procs for pid in _session_pids(p.pid) if rx.search(_cmdline(pid))]
+        if oldest and matches:
+            matches = [min(matches, key=_start_ticks)]
+        n = 0
+        for pid in matches:
+            try:
+                os.kill(pid, signal.SIGKILL)
+                n += 1
+            except ProcessLookupError:
+                pass
+        return n
+
     def wait_for_deployment(self, app_id: str, timeout_s: Optional[float] = None) -> None:
         app = self._get(app_id)
         if not app.deployed.wait(self.deploy_timeout_s if timeout_s is None else timeout_s):

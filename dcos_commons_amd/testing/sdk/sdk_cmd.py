@@ -266,6 +266,22 @@ def run_cli(cmd: str, print_output: bool = True, check: bool = False) -> Tuple[i
         rc, out, err = 0, f"Uninstalled package [{args[2]}]\n", ""
     elif args[:2] == ["task", "exec"]:
         rc, out, err = service_task_exec(None, args[2], " ".join(args[3:]))
+    elif args[:2] == ["task", "log"]:
+        # dcos task log [--completed] [--lines=N] [stderr] <task id or name>
+        lines = next((int(a.split("=", 1)[1]) for a in args if a.startswith("--lines=")), 10)
+        pos = [a for a in args[2:] if not a.startswith("--")]
+        stream = "stderr" if "stderr" in pos[1:] else "stdout"
+        task = pos[0]
+        views = [v for v in c.tasks(include_terminal=True) if v.id == task or v.name == task]
+        if views and c.executor == "process":
+            path = c.behavior.sandbox_of(views[-1].id)
+            try:
+                with open(os.path.join(path, stream), "r", encoding="utf-8", errors="replace") as f:
+                    rc, out, err = 0, "\n".join(f.read().splitlines()[-lines:]) + "\n", ""
+            except (OSError, TypeError) as e:
+                rc, out, err = 1, "", f"{e}\n"
+        else:
+            rc, out, err = 1, "", f"no task {task}\n"
     elif len(args) >= 2 and args[1].startswith("--name="):
         return svc_cli(args[0], args[1].split("=", 1)[1], " ".join(shlex.quote(a) for a in args[2:]),
                        print_output, False, check)

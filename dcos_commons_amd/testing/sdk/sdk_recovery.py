@@ -27,9 +27,10 @@ def check_permanent_recovery(package_name: str, service_name: str, pod_name: str
     others = {pod: set(sdk_tasks.get_task_ids(service_name, f"{pod}-")) for pod in pods - to_update}
     LOG.info("Replacing %s: tasks to replace %s, tasks to keep %s", pod_name, replaced, others)
     sdk_cmd.svc_cli(package_name, service_name, f"pod replace {pod_name}", check=True)
-    sdk_plan.wait_for_kicked_off_recovery(service_name, recovery_timeout_s)
-    sdk_plan.wait_for_completed_recovery(service_name, recovery_timeout_s)
+    # (no wait for a kicked-off recovery: on the local cluster it can start and complete between
+    # two polls; the relaunched tasks are the evidence)
     for pod, ids in replaced.items():
-        sdk_tasks.check_tasks_updated(service_name, f"{pod}-", ids)
+        sdk_tasks.check_tasks_updated(service_name, f"{pod}-", ids, recovery_timeout_s)
+    sdk_plan.wait_for_completed_recovery(service_name, recovery_timeout_s)
     for pod, ids in others.items():
         sdk_tasks.check_tasks_not_updated(service_name, f"{pod}-", ids)
