@@ -108,9 +108,17 @@ class LocalCluster:
         if executor == "process":
             from dcos_commons_amd.mesos.containerizer import ProcessTaskBehavior
 
+            from dcos_commons_amd.testing.cluster.marathon import REPO_ROOT
+
+            # tasks see this SDK's python package (what a fetched artifact provides on DC/OS: e.g.
+            # the MI355X readiness probe `python3 -m dcos_commons_amd.ops.gpu_health`) and the
+            # host's ROCm/HSA settings
+            task_env = {"PYTHONPATH": REPO_ROOT}
+            task_env.update({k: v for k, v in os.environ.items()
+                             if k.startswith(("HSA_", "ROCM_", "HIP_PLATFORM", "LD_LIBRARY_PATH"))})
             self.behavior = ProcessTaskBehavior(os.path.join(self.work_dir, "agents"),
                                                 secret_resolver=self.secrets.get, resolver=self.resolve,
-                                                artifact_resolver=self.resolve_artifact)
+                                                artifact_resolver=self.resolve_artifact, extra_env=task_env)
         elif executor == "synthetic":
             self.behavior = _SyntheticBehavior(finish_tasks)
         else:
