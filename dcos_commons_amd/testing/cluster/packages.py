@@ -31,6 +31,7 @@ from dcos_commons_amd.testing.cluster.marathon import REPO_ROOT, normalize_app_i
 
 LOGGER = logging.getLogger(__name__)
 DEFAULT_VERSION = "1.0.0-local"
+PREVIOUS_VERSION = "0.9.0-local"
 
 
 def flatten_options(options: Mapping, prefix: str = "") -> Dict[str, str]:
@@ -97,6 +98,9 @@ class LocalCosmos:
         self.cluster = cluster
         self._versions: Dict[str, List[PackageVersion]] = {}
         for name, udir in (packages if packages is not None else default_packages()).items():
+            # a "released" version and the one built from this tree (the stub universe): upgrade
+            # tests roll every task from one to the other (the version is in the task env)
+            self.register(name, udir, PREVIOUS_VERSION)
             self.register(name, udir)
         self.installed: Dict[str, InstalledService] = {}
 

@@ -49,12 +49,20 @@ def _update(package_name: str, service_name: str, to_version: Optional[str], to_
 def update_or_upgrade_or_downgrade(package_name: str, service_name: str, to_version: Optional[str],
                                    to_options: Dict[str, Any], expected_running_tasks: int,
                                    wait_for_deployment: bool = True, timeout_seconds: int = TIMEOUT_SECONDS) -> None:
+    from dcos_commons_amd.testing.sdk import sdk_marathon
+
     task_ids = sdk_tasks.get_task_ids(service_name, "")
     if to_version is None and not to_options:
         return
+    before = sdk_marathon.get_config(service_name).get("env", {})
     _update(package_name, service_name, to_version, to_options)
+    after = sdk_marathon.get_config(service_name).get("env", {})
+    # package coordinates alone do not touch tasks; anything else in the scheduler env may
+    ignore = {"PACKAGE_VERSION", "PACKAGE_BUILD_TIME_EPOCH_MS", "PACKAGE_BUILD_TIME_STR"}
+    changed = {k for k in set(before) | set(after) if k not in ignore and before.get(k) != after.get(k)}
     if wait_for_deployment:
-        sdk_tasks.check_tasks_updated(service_name, "", task_ids, timeout_seconds)
+        if changed:
+            sdk_tasks.check_tasks_updated(service_name, "", task_ids, timeout_seconds)
         sdk_plan.wait_for_completed_deployment(service_name, timeout_seconds)
         sdk_tasks.check_running(service_name, expected_running_tasks, timeout_seconds)
 

@@ -164,8 +164,10 @@ def test_operator_started_plans():
     r.run([Send.register(), Send.drive_plan("deploy"), Expect.that(sidecar, "sidecar plan waits for start"),
            Send.http("POST", "/v1/plans/sidecar/start", b"{}", 200),
            Send.drive_plan("sidecar"), Expect.plan_status("sidecar", Status.COMPLETE),
+           # the never-started "toxic" sidecar is known too: it shares the sidecar resource set,
+           # whose reservation is recorded on every task of the set
            Expect.known_tasks("hello-0-server", "hello-1-server", "hello-0-backup", "hello-1-backup",
-                              "hello-0-verify", "hello-1-verify")])
+                              "hello-0-verify", "hello-1-verify", "hello-0-toxic", "hello-1-toxic")])
 
 
 def test_update_plan_rolls_out_config_change():
