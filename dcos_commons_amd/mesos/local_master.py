@@ -612,6 +612,8 @@ class LocalMaster:
         if fw is None or not offers or any(o is None or o.framework_id != fid for o in offers) or \
                 len({o.agent_id for o in offers}) != 1:
             # invalid offers: every launched task is dropped
+            LOGGER.warning("ACCEPT of framework %s rejected: offers %s are invalid or no longer valid (%d operations "
+                           "dropped)", fid, offer_ids, len(ops))
             for op in ops:
                 for t in self._op_tasks(op):
                     self._deliver_synthetic(fid, t, P.TASK_DROPPED, P.TaskStatus.REASON_INVALID_OFFERS,

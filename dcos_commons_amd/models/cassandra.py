@@ -177,7 +177,9 @@ def main(argv=None) -> int:
     from dcos_commons_amd.utils import logging_utils
 
     logging_utils.configure()
-    SchedulerRunner.from_scheduler_builder(create_scheduler_builder(argv[0])).run()
+    from dcos_commons_amd.models import resolve_spec
+
+    SchedulerRunner.from_scheduler_builder(create_scheduler_builder(resolve_spec(argv[0], "cassandra"))).run()
     return 0
 
 

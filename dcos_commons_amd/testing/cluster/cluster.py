@@ -40,6 +40,9 @@ LOGGER = logging.getLogger(__name__)
 CLUSTER_DNS_SUFFIXES = (".thisdcos.directory", ".mesos", ".dcos")
 DEFAULT_REGION = "us-west-2"
 DEFAULT_ZONES = ("us-west-2a", "us-west-2b", "us-west-2c")
+# what a DC/OS private agent offers: everything above 1024 except the ports of the agent's own
+# services (ZooKeeper 2181/3888, Mesos agent 5051, adminrouter 8080-8081, ...)
+DCOS_AGENT_PORTS = ((1025, 2180), (2182, 3887), (3889, 5049), (5052, 8079), (8082, 8180), (8182, 32000))
 
 _current: Optional["LocalCluster"] = None
 _current_lock = threading.Lock()
@@ -126,6 +129,7 @@ class LocalCluster:
         self.executor = executor
         if agent_specs is None:
             agent_specs = [AgentSpec(hostname=f"10.0.0.{i + 1}", cpus=agent_cpus, mem=agent_mem, disk=agent_disk,
+                                     ports=DCOS_AGENT_PORTS,
                                      region=region, zone=zones[i % len(zones)] if zones else None,
                                      gpus=gpus_per_agent,
                                      attributes=({"gpu_vendor": "amd", "gpu_model": "MI355X"}

@@ -83,6 +83,7 @@ class _App:
     deployed: threading.Event = field(default_factory=threading.Event)
     lock: threading.Lock = field(default_factory=threading.Lock)
     supervisor: Optional[threading.Thread] = None
+    running_version: str = ""
 
 
 class LocalMarathon:
@@ -233,6 +234,23 @@ class LocalMarathon:
                 pass
         return "\n".join(out)
 
+    def history_log_tails(self, app_id: str, n: int = 40) -> str:
+        """Log tails of every scheduler process the app ever ran (also after it was destroyed)."""
+        with self._lock:
+            app = self._apps.get(normalize_app_id(app_id))
+        if app is None:
+            return ""
+        out = []
+        for t in app.history:
+            for name in ("stderr",):
+                try:
+                    with open(os.path.join(t.sandbox, name), "rb") as f:
+                        lines = f.read().decode("utf-8", "replace").splitlines()[-n:]
+                    out.append(f"--- {t.id} ({t.state}, exit {t.exit_code}) {name} ---\n" + "\n".join(lines))
+                except OSError:
+                    pass
+        return "\n".join(out)
+
     def shutdown(self) -> None:
         with self._lock:
             apps = list(self._apps.values())
@@ -293,6 +311,7 @@ class LocalMarathon:
                                     stdout=out, stderr=err, start_new_session=True)
         with app.lock:
             app.proc, app.task = proc, task
+            app.running_version = app.version
             app.history.append(task)
         LOGGER.info("Marathon started %s (%s, pid %d, api port %d)", app.id, tid, proc.pid, app.api_port)
 
@@ -310,7 +329,9 @@ class LocalMarathon:
             self._start(app)
             proc = app.proc
             while proc.poll() is None:
-                if not app.deployed.is_set() and self._api_up(app):
+                # only the process started for the current version completes a deployment (the
+                # previous one may still be serving while it is being stopped)
+                if not app.deployed.is_set() and app.running_version == app.version and self._api_up(app):
                     app.deployed.set()
                 if app.destroyed:
                     break

@@ -85,6 +85,10 @@ def uninstall(package_name: str, service_name: str, timeout_seconds: int = TIMEO
         return
     LOG.info("Uninstalling package=%s service=%s", package_name, service_name)
     c.cosmos.uninstall(service_name, timeout_s=timeout_seconds)
-    _verify_completed_uninstall(service_name)
+    try:
+        _verify_completed_uninstall(service_name)
+    except Exception:
+        LOG.error("Scheduler logs of %s:\n%s", service_name, c.marathon.history_log_tails(service_name, 60))
+        raise
     _dead_agent_hosts.clear()
     LOG.info("Uninstalled %s after %s", service_name, sdk_utils.pretty_duration(time.time() - start))
