@@ -103,6 +103,52 @@ class LocalCosmos:
             self.register(name, udir, PREVIOUS_VERSION)
             self.register(name, udir)
         self.installed: Dict[str, InstalledService] = {}
+        self.repositories: List[dict] = []
+
+    # -- repositories -------------------------------------------------------------------------
+    def add_repo(self, location: str, name: Optional[str] = None) -> List[PackageVersion]:
+        """``dcos package repo add``: register every release a universe repository holds (a stub
+        universe JSON file/URL, a ``.dcos`` bundle or a repository tree; see
+        ``tools.universe.package_manager``). Releases register in ``releaseVersion`` order, so the
+        newest one is what an install without ``--package-version`` gets. A ``.dcos`` bundle's
+        artifacts are staged into the cluster's artifact store, where the fetcher finds them by
+        file name (the air-gapped path: nothing is downloaded)."""
+        from dcos_commons_amd.tools.universe import package_manager as pm
+
+        definitions = sorted(pm.load_repository(location), key=lambda d: int(d.get("releaseVersion", 0)))
+        base = os.path.join(self.cluster.work_dir, "universe")
+        added = []
+        for d in definitions:
+            pdir = os.path.join(base, d["name"], str(d.get("releaseVersion", 0)) + "-" + d["version"])
+            os.makedirs(pdir, exist_ok=True)
+            for fname, text in pm.files_from_package(d).items():
+                with open(os.path.join(pdir, fname), "w", encoding="utf-8") as f:
+                    f.write(text)
+            added.append(self.register(d["name"], pdir, d["version"]))
+        if location.endswith(".dcos"):
+            self._stage_bundle_resources(location, os.path.join(base, "resources"))
+        self.repositories.append({"name": name or f"repo-{len(self.repositories)}", "uri": location,
+                                  "packages": [f"{p.name}:{p.version}" for p in added]})
+        return added
+
+    def _stage_bundle_resources(self, bundle: str, out_dir: str) -> None:
+        import zipfile
+
+        from dcos_commons_amd.tools.universe.package_manager import RESOURCES_DIR
+
+        with zipfile.ZipFile(bundle) as z:
+            for member in z.namelist():
+                if not member.startswith(RESOURCES_DIR + "/") or member.endswith("/"):
+                    continue
+                base = os.path.basename(member)
+                dest = os.path.join(out_dir, base)
+                os.makedirs(out_dir, exist_ok=True)
+                with z.open(member) as src, open(dest, "wb") as dst:
+                    dst.write(src.read())
+                self.cluster.register_artifact(base, dest)
+
+    def remove_repo(self, name: str) -> None:
+        self.repositories = [r for r in self.repositories if r["name"] != name]
 
     # -- registry -------------------------------------------------------------------------
     def register(self, name: str, universe_dir: str, version: str = DEFAULT_VERSION) -> PackageVersion:

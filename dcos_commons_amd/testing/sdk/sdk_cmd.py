@@ -264,6 +264,17 @@ def run_cli(cmd: str, print_output: bool = True, check: bool = False) -> Tuple[i
         app_id = next((a.split("=", 1)[1] for a in args if a.startswith("--app-id=")), args[2])
         c.cosmos.uninstall(app_id)
         rc, out, err = 0, f"Uninstalled package [{args[2]}]\n", ""
+    elif args[:3] == ["package", "repo", "add"]:
+        # dcos package repo add [--index=N] <name> <uri>
+        pos = [a for a in args[3:] if not a.startswith("--")]
+        added = c.cosmos.add_repo(pos[1], pos[0])
+        rc, out, err = 0, "".join(f"Added {p.name} {p.version}\n" for p in added), ""
+    elif args[:3] == ["package", "repo", "remove"]:
+        c.cosmos.remove_repo(args[3])
+        rc, out, err = 0, "", ""
+    elif args[:3] == ["package", "repo", "list"]:
+        rc, out, err = 0, json.dumps({"repositories": [{"name": r["name"], "uri": r["uri"]}
+                                                       for r in c.cosmos.repositories]}) + "\n", ""
     elif args[:2] == ["task", "exec"]:
         rc, out, err = service_task_exec(None, args[2], " ".join(args[3:]))
     elif args[:2] == ["task", "log"]:
