@@ -444,7 +444,10 @@ class LocalMaster:
             existing = self.frameworks.get(fid)
             fw = _Framework(fid, info, driver, roles)
             if existing is not None:
-                fw.filters = {}
+                # failover: offers outstanding to the previous scheduler instance are recovered
+                # (the new instance never saw them; Mesos rescinds them on failover)
+                for oid in [o.id for o in self.offers.values() if o.framework_id == fid]:
+                    self._return_offer(oid, 0)
             self.frameworks[fid] = fw
             driver._framework_id = fid
             driver._deliver(lambda s: s.registered(driver, P.FrameworkID(value=fid), self.master_info))

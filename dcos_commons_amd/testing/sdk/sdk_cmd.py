@@ -277,6 +277,18 @@ def run_cli(cmd: str, print_output: bool = True, check: bool = False) -> Tuple[i
                                                        for r in c.cosmos.repositories]}) + "\n", ""
     elif args[:2] == ["task", "exec"]:
         rc, out, err = service_task_exec(None, args[2], " ".join(args[3:]))
+    elif args[:2] == ["task", "ls"]:
+        # dcos task ls <task id or name> [path]: the sandbox listing of the newest matching task
+        pos = [a for a in args[2:] if not a.startswith("--")]
+        views = [v for v in c.tasks(include_terminal=True) if v.id == pos[0] or v.name == pos[0]]
+        path = c.behavior.sandbox_of(views[-1].id) if views and c.executor == "process" else None
+        if path is None:
+            rc, out, err = 1, "", f"no task {pos[0]}\n"
+        else:
+            try:
+                rc, out, err = 0, "  ".join(sorted(os.listdir(os.path.join(path, *pos[1:2])))) + "\n", ""
+            except OSError as e:
+                rc, out, err = 1, "", f"{e}\n"
     elif args[:2] == ["task", "log"]:
         # dcos task log [--completed] [--lines=N] [stderr] <task id or name>
         lines = next((int(a.split("=", 1)[1]) for a in args if a.startswith("--lines=")), 10)

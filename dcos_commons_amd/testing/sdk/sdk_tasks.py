@@ -8,7 +8,7 @@ from __future__ import annotations
 
 import logging
 import time
-from typing import Dict, Iterable, List, Optional
+from typing import Any, Dict, Iterable, List, Optional
 
 LOG = logging.getLogger(__name__)
 DEFAULT_TIMEOUT_SECONDS = 120
@@ -103,9 +103,9 @@ def get_task_ids(service_name: str, task_prefix: str = "") -> List[str]:
     return sorted(t.id for t in get_service_tasks(service_name, task_prefix))
 
 
-def get_all_status_history(task_name: str, with_completed_tasks: bool = True) -> List[str]:
-    """Every status (``TASK_STARTING``, ``TASK_RUNNING``, ...) of every instance of ``task_name``,
-    oldest first."""
+def get_all_status_history(task_name: str, with_completed_tasks: bool = True) -> List[Dict[str, Any]]:
+    """Every status of every instance of ``task_name``, oldest first, as the state-summary JSON
+    shows them: ``{"state": "TASK_RUNNING", "timestamp": ...}``."""
     statuses = []
     for v in _cluster().tasks(include_terminal=with_completed_tasks):
         if v.name == task_name:
@@ -113,7 +113,7 @@ def get_all_status_history(task_name: str, with_completed_tasks: bool = True) ->
     statuses.sort(key=lambda s: s.timestamp)
     from dcos_commons_amd.mesos import protos as P
 
-    return [P.TaskState.Name(s.state) for s in statuses]
+    return [{"state": P.TaskState.Name(s.state), "timestamp": s.timestamp} for s in statuses]
 
 
 def get_failed_task_count(service_name: str, retry: bool = False) -> int:

@@ -123,7 +123,7 @@ def test_pods_restart_graceful_shutdown():
     # the SIGTERM reached the task's trap (its message, not the echo command line, is in the log)
     _, out, _ = sdk_cmd.run_cli(f"task log --completed --lines=1000 {world_ids[0]}")
     assert any("all clean" in line and "echo" not in line for line in out.splitlines()), out
-    statuses = sdk_tasks.get_all_status_history("world-0-server")
+    statuses = [s["state"] for s in sdk_tasks.get_all_status_history("world-0-server")]
     assert "TASK_KILLED" in statuses
 
 

@@ -60,9 +60,10 @@ def test_taskcfg_routing():
         t = _launched(sim)
         hello = {v.name: v.value for v in t["hello-0-server"].command.environment.variables}
         world = {v.name: v.value for v in t["world-0-server"].command.environment.variables}
-        assert hello["GREETING"] == "hi" and hello["TARGET"] == "everyone"  # TASKCFG_HELLO_* beats task env
+        assert hello["GREETING"] == "hi" and hello["TARGET"] == "everyone"  # TASKCFG_HELLO_*: hello only
         assert world["GREETING"] == "hi" and "TARGET" not in world
-    _run("taskcfg.yml", check)
+        assert hello["OUTPUT_FILENAME"] == "out" and world["SLEEP_DURATION"] == "5"
+    _run("taskcfg.yml", check, env={"TASKCFG_ALL_OUTPUT_FILENAME": "out", "TASKCFG_ALL_SLEEP_DURATION": "5"})
 
 
 def test_discovery_prefix_and_kill_grace_and_uris():

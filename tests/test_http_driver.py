@@ -212,6 +212,34 @@ def test_stream_loss_disconnects_or_fails_over(cluster):
         d2.stop()
 
 
+def test_failover_recovers_offers_held_by_the_previous_instance(cluster):
+    """A scheduler that re-subscribes with its FrameworkID while the master still counts offers as
+    outstanding to the old instance gets those resources offered again (Mesos rescinds them on
+    failover); before, a restarted scheduler could wait forever for an agent's resources."""
+    lm, hm = cluster
+    rec = Recorder()
+    d = V1HttpSchedulerDriver(hm.url, rec, P.FrameworkInfo(name="fw", role="r"))
+    d.start()
+    fid = rec.wait_for("registered")[0][1]
+    rec.wait_for("offers")
+    d.suppress_offers()
+    # the old instance disappears without its stream being noticed: offers stay outstanding
+    d._tearing_down = True
+    d.stop(failover=True)
+    assert any(o.framework_id == fid for o in lm.offers.values())
+    rec2 = Recorder()
+    info = P.FrameworkInfo(name="fw", role="r")
+    info.id.value = fid
+    d2 = V1HttpSchedulerDriver(hm.url, rec2, info)
+    d2.start()
+    try:
+        rec2.wait_for("registered")
+        offers = rec2.wait_for("offers")[0][1]
+        assert offers and offers[0].hostname == "h0"
+    finally:
+        d2.stop()
+
+
 def test_subscribe_rejected_calls_error():
     rec = Recorder()
     d = V1HttpSchedulerDriver("http://127.0.0.1:9", rec, P.FrameworkInfo(name="fw"), backoff_s=0.01,
