@@ -83,7 +83,7 @@ class AgentSpec:
     attributes: Dict[str, str] = field(default_factory=dict)
     zone: Optional[str] = None
     region: Optional[str] = None
-    mount_disks: Tuple[Tuple[str, float], ...] = ()
+    mount_disks: Tuple[tuple, ...] = ()  # (root, size) or (root, size, profile)
     pre_reserved: Tuple[Tuple[str, str, float], ...] = ()  # (role, resource name, amount)
 
     def resources(self) -> List[P.Resource]:
@@ -95,10 +95,15 @@ class AgentSpec:
             out.append(ranges("ports", self.ports))
         if self.gpus:
             out.append(scalar("gpus", float(self.gpus)))
-        for root, size in self.mount_disks:
+        for disk in self.mount_disks:
+            # (root, size) or (root, size, profile): a profiled disk comes from a CSI volume
+            # profile (DC/OS storage "volume_profile"), which MOUNT volumes may ask for by name
+            root, size = disk[0], disk[1]
             r = scalar("disk", size)
             r.disk.source.type = P.Resource.DiskInfo.Source.MOUNT
             r.disk.source.mount.root = root
+            if len(disk) > 2 and disk[2]:
+                r.disk.source.profile = disk[2]
             out.append(r)
         # statically pre-reserved resources come out of the unreserved pool
         bag = ResourceBag(out)
@@ -171,6 +176,8 @@ class _Task:
     gpu_devices: List[int]
     status: P.TaskStatus
     epoch: int = 0  # bumps on kill/failure so stale timers are ignored
+    # the task's addresses as its statuses report them (``container_status.network_infos``)
+    networks: List[P.NetworkInfo] = field(default_factory=list)
 
 
 @dataclass
@@ -179,6 +186,10 @@ class _Executor:
     framework_id: str
     resources: List[P.Resource]
     tasks: Set[str] = field(default_factory=set)
+
+
+# CNI networks that map container ports to host ports (the container is reached on the agent's address)
+BRIDGE_NETWORKS = ("mesos-bridge", "bridge")
 
 
 class _Agent:
@@ -192,6 +203,43 @@ class _Agent:
         self.free_gpus: List[int] = list(devices)
         self.active = True
         self.check_runner = None  # per-agent check executor (e.g. a remote GPU agent)
+        self.index = 0            # position among the master's agents (overlay subnet 9.0.<index>.0/24)
+        self._overlay_ips = itertools.count(2)
+
+    @property
+    def ip(self) -> str:
+        """The agent's address: its hostname when that is an IPv4 literal (``10.0.0.3``)."""
+        parts = self.spec.hostname.split(".")
+        if len(parts) == 4 and all(p.isdigit() and int(p) < 256 for p in parts):
+            return self.spec.hostname
+        return "127.0.0.1"
+
+    def task_networks(self, container: Optional[P.ContainerInfo]) -> List[P.NetworkInfo]:
+        """Addresses of a container joining ``container.network_infos``, as Mesos reports them.
+
+        Host networking (no network infos) reports the agent's address with no network name;
+        bridge CNI networks with port mappings (``mesos-bridge``) name the network and are reached
+        on the agent's address; any other named network is a virtual (overlay) network: the
+        container gets its own address from the agent's overlay subnet ``9.0.<agent index>.0/24``
+        and the status names the network and carries its labels (DC/OS ``dcos`` overlay,
+        reference ``overlay.yml``)."""
+        out: List[P.NetworkInfo] = []
+        for ni in (container.network_infos if container is not None else ()):
+            if not ni.name:
+                continue
+            n = P.NetworkInfo(name=ni.name)
+            if ni.name in BRIDGE_NETWORKS:
+                n.ip_addresses.add(ip_address=self.ip)
+            else:
+                n.ip_addresses.add(ip_address=f"9.0.{self.index % 256}.{next(self._overlay_ips) % 254 + 1}")
+            if ni.HasField("labels"):
+                n.labels.CopyFrom(ni.labels)
+            out.append(n)
+        if not out:
+            n = P.NetworkInfo()
+            n.ip_addresses.add(ip_address=self.ip)
+            out.append(n)
+        return out
 
     def info_attributes(self) -> List[P.Attribute]:
         return [text_attribute(k, v) for k, v in sorted(self.spec.attributes.items())]
@@ -303,6 +351,7 @@ class LocalMaster:
             aid = f"agent-{len(self.agents)}-{uuid.uuid4().hex[:6]}"
             self.agents[aid] = _Agent(aid, spec)
             self.agents[aid].check_runner = check_runner
+            self.agents[aid].index = len(self.agents)
             self._allocate()
             return aid
         return self.call(do)
@@ -738,6 +787,9 @@ class LocalMaster:
             if eid:
                 st.executor_id.value = eid
             task = _Task(t, fw.id, eid, agent.id, rs, devices, st)
+            task.networks = agent.task_networks(
+                executor.container if executor is not None and executor.HasField("container") else
+                (t.container if t.HasField("container") else None))
             agent.tasks[t.task_id.value] = task
             if eid:
                 agent.executors[key].tasks.add(t.task_id.value)
@@ -907,7 +959,10 @@ class LocalMaster:
             setattr(st, k, v)
         if task.gpu_devices:
             st.labels.labels.add(key="gpu_devices", value=",".join(str(d) for d in task.gpu_devices))
-        st.container_status.network_infos.add().ip_addresses.add(ip_address="127.0.0.1")
+        if task.networks:
+            st.container_status.network_infos.extend(task.networks)
+        else:
+            st.container_status.network_infos.add().ip_addresses.add(ip_address="127.0.0.1")
         st.uuid = uuid.uuid4().bytes
         task.status = st
         if state in TERMINAL:

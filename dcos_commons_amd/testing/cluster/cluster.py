@@ -99,7 +99,8 @@ class LocalCluster:
                  region: str = DEFAULT_REGION, zones: Sequence[str] = DEFAULT_ZONES, gpus_per_agent: int = 0,
                  agent_cpus: float = 8.0, agent_mem: float = 32768.0, agent_disk: float = 65536.0,
                  packages: Optional[Dict[str, str]] = None, scheduler_env: Optional[Dict[str, str]] = None,
-                 finish_tasks: Sequence[str] = (), dcos_version: str = "1.13.0", keep_work_dir: bool = False):
+                 finish_tasks: Sequence[str] = (), dcos_version: str = "1.13.0", keep_work_dir: bool = False,
+                 mount_disks: Sequence[tuple] = ()):
         self.work_dir = os.path.abspath(work_dir or tempfile.mkdtemp(prefix="sdk-cluster-"))
         self._own_work_dir = work_dir is None and not keep_work_dir
         self.region = region
@@ -131,7 +132,7 @@ class LocalCluster:
             agent_specs = [AgentSpec(hostname=f"10.0.0.{i + 1}", cpus=agent_cpus, mem=agent_mem, disk=agent_disk,
                                      ports=DCOS_AGENT_PORTS,
                                      region=region, zone=zones[i % len(zones)] if zones else None,
-                                     gpus=gpus_per_agent,
+                                     gpus=gpus_per_agent, mount_disks=tuple(mount_disks),
                                      attributes=({"gpu_vendor": "amd", "gpu_model": "MI355X"}
                                                  if gpus_per_agent else {}))
                            for i in range(agents)]
@@ -250,7 +251,8 @@ class LocalCluster:
 
     def frameworks(self, include_inactive: bool = False) -> List[dict]:
         def do():
-            return [{"id": fid, "name": fw.info.name, "active": fw.connected, "roles": sorted(fw.roles)}
+            return [{"id": fid, "name": fw.info.name, "active": fw.connected, "roles": sorted(fw.roles),
+                     "webui_url": fw.info.webui_url}
                     for fid, fw in self.master.frameworks.items() if include_inactive or fw.connected]
         return self.master.call(do)
 
@@ -293,6 +295,34 @@ class LocalCluster:
                 if role is None or effective_role(r) == role:
                     out.append((a["hostname"], r))
         return out
+
+    def dns_enumerate(self) -> dict:
+        """Mesos-DNS ``/v1/enumerate``: per framework, each running task's A record
+        ``<task>.<framework>.mesos.`` and one SRV record per named discovery port,
+        ``_<port name>._<discovery name>._<protocol>.<framework>.mesos.``, pointing at the task's
+        address. Tasks without ports only get the A record."""
+        def do():
+            fws: Dict[str, dict] = {}
+            for fid, fw in self.master.frameworks.items():
+                fws[fid] = {"name": fw.info.name, "tasks": []}
+            for a in self.master.agents.values():
+                for t in a.tasks.values():
+                    if P.TaskState.Value("TASK_RUNNING") != t.status.state or t.framework_id not in fws:
+                        continue
+                    fw_name = fws[t.framework_id]["name"].replace("/", "")
+                    ip = next((x.ip_address for n in t.networks for x in n.ip_addresses), a.ip)
+                    d = t.info.discovery if t.info.HasField("discovery") else None
+                    dns_name = d.name if d is not None and d.name else t.info.name
+                    records = [{"name": f"{dns_name}.{fw_name}.mesos.", "host": ip, "rtype": "A"}]
+                    for port in (d.ports.ports if d is not None else ()):
+                        if not port.name:
+                            continue
+                        proto = port.protocol or "tcp"
+                        records.append({"name": f"_{port.name}._{dns_name}._{proto}.{fw_name}.mesos.",
+                                        "host": f"{ip}:{port.number}", "rtype": "SRV"})
+                    fws[t.framework_id]["tasks"].append({"name": t.info.name, "records": records})
+            return {"frameworks": list(fws.values())}
+        return self.master.call(do)
 
     def zk_children(self, path: str = "/") -> List[str]:
         from dcos_commons_amd.storage.zookeeper import ZkClient
@@ -342,6 +372,10 @@ class LocalCluster:
         n = 0
         if agent_host in (None, "127.0.0.1", "localhost"):
             n += self.marathon.kill_with_pattern(pattern, oldest=oldest)
+            if n and oldest:
+                return n
+        else:   # a scheduler placed on this agent by its app constraints
+            n += self.marathon.kill_with_pattern(pattern, oldest=oldest, host=agent_host)
             if n and oldest:
                 return n
         if self.executor == "process" and agent_host not in ("127.0.0.1", "localhost"):

@@ -193,15 +193,17 @@ class LocalMarathon:
         os.killpg(proc.pid, sig)
         return task.id
 
-    def kill_with_pattern(self, pattern: str, oldest: bool = False) -> int:
-        """``pkill -9 -f`` over the scheduler processes (and their children)."""
+    def kill_with_pattern(self, pattern: str, oldest: bool = False, host: Optional[str] = None) -> int:
+        """``pkill -9 -f`` over the scheduler processes (and their children); with ``host``, only
+        over those of schedulers placed on that agent."""
         import re
 
         from dcos_commons_amd.mesos.containerizer import _cmdline, _session_pids, _start_ticks
 
         rx = re.compile(pattern)
         with self._lock:
-            procs = [a.proc for a in self._apps.values() if a.proc is not None and a.proc.poll() is None]
+            procs = [a.proc for a in self._apps.values() if a.proc is not None and a.proc.poll() is None
+                     and (host is None or (a.task is not None and a.task.host == host))]
         matches = [pid for p in procs for pid in _session_pids(p.pid) if rx.search(_cmdline(pid))]
         if oldest and matches:
             matches = [min(matches, key=_start_ticks)]
@@ -303,7 +305,7 @@ class LocalMarathon:
         tid = f"{scheduler_task_prefix(app.id)}.{uuid.uuid4()}"
         sandbox = os.path.join(self.cluster.work_dir, "marathon", app.id.strip("/").replace("/", "_"), tid)
         os.makedirs(sandbox, exist_ok=True)
-        task = MarathonTask(tid, app.id, "127.0.0.1", [app.api_port], sandbox, time.time())
+        task = MarathonTask(tid, app.id, self._place(app), [app.api_port], sandbox, time.time())
         env = self._environment(app, task)
         cmd = app.definition.get("cmd") or ""
         with open(os.path.join(sandbox, "stdout"), "ab") as out, open(os.path.join(sandbox, "stderr"), "ab") as err:
@@ -314,6 +316,33 @@ class LocalMarathon:
             app.running_version = app.version
             app.history.append(task)
         LOGGER.info("Marathon started %s (%s, pid %d, api port %d)", app.id, tid, proc.pid, app.api_port)
+
+    def _place(self, app: _App) -> str:
+        """The agent the scheduler task runs on. Without app ``constraints`` that is the loopback
+        host (the master node of the stand-in); with them, the first active agent matching all of
+        ``[field, LIKE|UNLIKE|CLUSTER|IS, value]`` on ``hostname`` or an agent attribute
+        (Marathon's constraint operators; UNIQUE/GROUP_BY/MAX_PER hold for a single instance)."""
+        import re
+
+        constraints = app.definition.get("constraints") or []
+        if not constraints:
+            return "127.0.0.1"
+        for a in sorted(self.cluster.agents(), key=lambda a: a["hostname"]):
+            if not a["active"]:
+                continue
+            ok = True
+            for c in constraints:
+                field, op = c[0], c[1].upper()
+                value = c[2] if len(c) > 2 else None
+                actual = a["hostname"] if field == "hostname" else a["attributes"].get(field)
+                if op in ("LIKE", "UNLIKE"):
+                    hit = actual is not None and re.fullmatch(value, actual) is not None
+                    ok &= hit if op == "LIKE" else not hit
+                elif op in ("CLUSTER", "IS"):
+                    ok &= actual == value
+            if ok:
+                return a["hostname"]
+        raise RuntimeError(f"no agent satisfies the constraints {constraints} of {app.id}")
 
     def _api_up(self, app: _App) -> bool:
         try:

@@ -90,8 +90,10 @@ def render_marathon_app(universe_dir: str, options: Optional[Mapping[str, str]] 
         missing = [m for m in missing if not m.name.startswith("sha256:")]
         T.validate_missing_values("universe/resource.json", rp, missing)
         flatten_tree("resource", json.loads(rendered), params)
-    # caller options land inside JSON strings too: escape quotes like the defaults
-    params.update({k: _scalar(v).replace('"', '\\"') for k, v in (options or {}).items()})
+    # caller options land inside JSON strings too: escape quotes like the defaults (arrays and
+    # objects are rendered as raw JSON values, e.g. the scheduler's ``constraints``)
+    params.update({k: _scalar(v) if isinstance(v, (list, dict)) else _scalar(v).replace('"', '\\"')
+                   for k, v in (options or {}).items()})
     params.update(build_params)
     params.update(MARATHON_TEMPLATE_PARAMS)
     params.update(package_params or {})

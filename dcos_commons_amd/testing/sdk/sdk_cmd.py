@@ -129,9 +129,14 @@ def _state_summary() -> dict:
                "reserved_resources": by_agent.get(a["hostname"], {}),
                "domain": {"fault_domain": {"region": {"name": a["region"]}, "zone": {"name": a["zone"]}}},
                "attributes": a["attributes"]} for a in c.agents()]
-    frameworks = [{"id": f["id"], "name": f["name"], "active": f["active"], "roles": f["roles"]}
+    frameworks = [{"id": f["id"], "name": f["name"], "active": f["active"], "roles": f["roles"],
+                   "webui_url": f.get("webui_url", "")}
                   for f in c.frameworks()]
-    return {"slaves": slaves, "frameworks": frameworks}
+    out = {"slaves": slaves, "frameworks": frameworks}
+    if c.master.domain is not None:
+        fd = c.master.domain.fault_domain
+        out["domain"] = {"fault_domain": {"region": {"name": fd.region.name}, "zone": {"name": fd.zone.name}}}
+    return out
 
 
 def cluster_request(method: str, cluster_path: str, retry: bool = True, raise_on_error: bool = True,
@@ -153,6 +158,8 @@ def cluster_request(method: str, cluster_path: str, retry: bool = True, raise_on
         elif path in ("/mesos/tasks", "/mesos/master/tasks"):
             body = {"tasks": [{"id": t.id, "name": t.name, "state": t.state, "framework_id": t.framework_id,
                                "slave_id": t.agent_id} for t in c.tasks(include_terminal=True)]}
+        elif path in ("/mesos_dns/v1/enumerate", "/mesos-dns/v1/enumerate"):
+            body = c.dns_enumerate()
         elif path == "/dcos-metadata/dcos-version.json":
             body = {"version": c.dcos_version, "dcos-variant": "open"}
         elif path.startswith("/marathon/v2/apps"):
@@ -350,6 +357,18 @@ def marathon_task_exec(task_name: str, cmd: str, print_output: bool = True) -> T
             return _run(["bash", "-c", cmd], print_output, False, env=None) if sandbox is None else \
                 _run(["bash", "-c", f"cd {shlex.quote(sandbox)} && {cmd}"], print_output, False)
     return 1, "", f"no marathon task {task_name}\n"
+
+
+def master_ssh(cmd: str, timeout_seconds: int = 60, print_output: bool = True) -> Tuple[int, str, str]:
+    """Commands the tests run on the master node. The master's services are in-process here:
+    ``curl localhost:8123/v1/enumerate`` (Mesos-DNS) is answered from the cluster's DNS view;
+    anything else runs as a local shell command."""
+    if "8123/v1/enumerate" in cmd:
+        out = json.dumps(_cluster().dns_enumerate())
+        if print_output:
+            LOG.info("(SDK) master: %s -> %s", cmd, out[:1000])
+        return 0, out, ""
+    return _run(["bash", "-c", cmd], print_output, False, timeout_seconds)
 
 
 def get_task_sandbox_path(task_id: str) -> str:

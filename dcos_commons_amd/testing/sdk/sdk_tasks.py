@@ -105,15 +105,23 @@ def get_task_ids(service_name: str, task_prefix: str = "") -> List[str]:
 
 def get_all_status_history(task_name: str, with_completed_tasks: bool = True) -> List[Dict[str, Any]]:
     """Every status of every instance of ``task_name``, oldest first, as the state-summary JSON
-    shows them: ``{"state": "TASK_RUNNING", "timestamp": ...}``."""
+    shows them: ``{"state": "TASK_RUNNING", "timestamp": ..., "container_status": {"network_infos": [...]}}``."""
     statuses = []
     for v in _cluster().tasks(include_terminal=with_completed_tasks):
         if v.name == task_name:
             statuses.extend(v.statuses)
     statuses.sort(key=lambda s: s.timestamp)
+    from google.protobuf import json_format
+
     from dcos_commons_amd.mesos import protos as P
 
-    return [{"state": P.TaskState.Name(s.state), "timestamp": s.timestamp} for s in statuses]
+    out = []
+    for s in statuses:
+        d = {"state": P.TaskState.Name(s.state), "timestamp": s.timestamp}
+        if s.HasField("container_status"):
+            d["container_status"] = json_format.MessageToDict(s.container_status, preserving_proto_field_name=True)
+        out.append(d)
+    return out
 
 
 def get_failed_task_count(service_name: str, retry: bool = False) -> int:

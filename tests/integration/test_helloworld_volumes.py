@@ -1,0 +1,145 @@
+"""helloworld volume scenarios on the local cluster.
+
+Reference: frameworks/helloworld/tests/{test_executor_volumes.py, test_host_volumes.py,
+test_mount_volumes.py, test_profile_mount_volumes.py}. A pod-level (executor) volume is shared by
+the pod's tasks and survives a task relaunch; host volumes expose agent paths inside the task; a
+MOUNT volume takes a whole agent disk and a task relaunched in place gets the same disk and its
+data back; a volume that asks for a disk profile only lands on disks of that profile.
+"""
+import json
+
+import pytest
+
+from dcos_commons_amd.testing.sdk import sdk_cmd, sdk_install, sdk_plan, sdk_tasks, sdk_utils
+from tests.integration import hw_config as config
+from tests.integration.conftest import make_cluster, needs_cli
+
+# every agent: one plain 2 GB disk and one 1 GB disk of the "fast-nvme" profile
+MOUNT_DISKS = (("/dcos/volume0", 2000.0), ("/dcos/volume1", 1000.0, "fast-nvme"))
+
+
+@pytest.fixture(scope="module")
+def local_cluster():
+    c = make_cluster(mount_disks=MOUNT_DISKS)
+    yield c
+    c.shutdown()
+
+
+pytestmark = pytest.mark.usefixtures("local_cluster")
+
+
+def _pod_info(pod):
+    return sdk_cmd.service_request("GET", config.SERVICE_NAME, f"/v1/pod/{pod}/info").json()
+
+
+def _volumes(task_info):
+    """(container path, persistence id, size, source) of every persistent volume of a task info
+    (its own resources and its executor's)."""
+    out = []
+    for r in task_info.get("resources", []) + task_info.get("executor", {}).get("resources", []):
+        disk = r.get("disk", {})
+        if "persistence" in disk:
+            out.append((disk["volume"]["containerPath"], disk["persistence"]["id"], r["scalar"]["value"],
+                        disk.get("source", {})))
+    return out
+
+
+def _log(task_name):
+    rc, out, _ = sdk_cmd.run_cli(f"task log --lines=50 {task_name}", print_output=False)
+    assert rc == 0
+    return out
+
+
+def test_executor_volume_shared_and_kept_across_relaunch():
+    sdk_install.install(config.PACKAGE_NAME, config.SERVICE_NAME, 2,
+                        additional_options={"service": {"yaml": "executor_volume"}, "hello": {"count": 2}})
+    try:
+        plan = sdk_plan.get_deployment_plan(config.SERVICE_NAME)
+        assert [p["name"] for p in plan["phases"]] == ["hello"]
+        assert [s["name"] for s in plan["phases"][0]["steps"]] == \
+            ["hello-0:[writer]", "hello-0:[server]", "hello-1:[writer]", "hello-1:[server]"]
+        # the writer (ONCE) wrote into the pod volume, the server read it from the same pod volume
+        for i in range(2):
+            assert "data" in _log(f"hello-{i}-server").split()
+            info = {t["info"]["name"]: t["info"] for t in _pod_info(f"hello-{i}")}
+            # (the writer's executor exited with its task group; the server's executor carries the
+            # same reserved pod volume)
+            pod_vols = [v for v in _volumes(info[f"hello-{i}-server"]) if v[0] == "pod-data"]
+            assert len(pod_vols) == 1 and pod_vols[0][2] == 64
+            assert [v for v in _volumes(info[f"hello-{i}-writer"]) if v[0] == "pod-data"] == pod_vols
+            assert [v[0] for v in _volumes(info[f"hello-{i}-server"]) if v[0] != "pod-data"] == ["task-data"]
+        old = sdk_tasks.get_service_tasks(config.SERVICE_NAME, "hello-0-server")[0]
+        vols_before = sorted(_volumes(next(t["info"] for t in _pod_info("hello-0")
+                                           if t["info"]["name"] == "hello-0-server")))
+        assert sdk_cmd.kill_task_with_pattern("pod-data/file", agent_host=old.host)
+        sdk_tasks.check_task_relaunched("hello-0-server", old.id)
+        sdk_plan.wait_for_completed_recovery(config.SERVICE_NAME)
+        new = sdk_tasks.get_service_tasks(config.SERVICE_NAME, "hello-0-server")[0]
+        assert new.host == old.host
+        # relaunched in place: same volumes, and the file the writer left is still there
+        assert sorted(_volumes(next(t["info"] for t in _pod_info("hello-0")
+                                    if t["info"]["name"] == "hello-0-server"))) == vols_before
+
+        @sdk_utils.retry(timeout_s=30, interval_s=0.5)
+        def reread():
+            assert _log("hello-0-server").split().count("data") >= 1
+        reread()
+    finally:
+        sdk_install.uninstall(config.PACKAGE_NAME, config.SERVICE_NAME)
+
+
+def test_host_volume_mounts():
+    sdk_install.install(config.PACKAGE_NAME, config.SERVICE_NAME, 1,
+                        additional_options={"service": {"yaml": "host-volume"}})
+    try:
+        info = _pod_info("hello-0")[0]["info"]
+        vols = {v["containerPath"]: v for v in info["container"]["volumes"]}
+        assert vols["host-etc"]["hostPath"] == "/etc" and vols["host-etc"]["mode"] == "RO"
+        assert vols["host-tmp"]["mode"] == "RW"
+
+        @sdk_utils.retry(timeout_s=30, interval_s=0.5)
+        def read_group():
+            rc, out, _ = sdk_cmd.service_task_exec(config.SERVICE_NAME, "hello-0-server", "cat host-etc/group")
+            assert rc == 0 and any(line.startswith("root:") for line in out.splitlines()), out
+        read_group()
+        rc, out, _ = sdk_cmd.service_task_exec(config.SERVICE_NAME, "hello-0-server", "ls host-tmp/x")
+        assert rc == 0, out
+    finally:
+        sdk_install.uninstall(config.PACKAGE_NAME, config.SERVICE_NAME)
+
+
+@needs_cli
+def test_pod_mount_volume_survives_task_kill():
+    sdk_install.install(config.PACKAGE_NAME, config.SERVICE_NAME, 2,
+                        additional_options={"service": {"yaml": "pod-mount-volume"}, "hello": {"count": 2}})
+    try:
+        rc, out, _ = sdk_cmd.svc_cli(config.PACKAGE_NAME, config.SERVICE_NAME, "pod info hello-0", print_output=False)
+        assert rc == 0
+        task = json.loads(out)[0]["info"]
+        (path, pid, size, source), = _volumes(task)
+        # the whole plain disk, not the profiled one
+        assert path == "mount-data" and size == 2000.0
+        assert source["type"] == "MOUNT" and source["mount"]["root"] == "/dcos/volume0" and "profile" not in source
+        old = sdk_tasks.get_service_tasks(config.SERVICE_NAME, "hello-0-server")[0]
+        sdk_cmd.service_task_exec(config.SERVICE_NAME, "hello-0-server", "echo kept > mount-data/marker")
+        assert sdk_cmd.kill_task_with_pattern("df mount-data", agent_host=old.host)
+        sdk_tasks.check_task_relaunched("hello-0-server", old.id)
+        sdk_plan.wait_for_completed_recovery(config.SERVICE_NAME)
+        rc, out, _ = sdk_cmd.svc_cli(config.PACKAGE_NAME, config.SERVICE_NAME, "pod info hello-0", print_output=False)
+        assert _volumes(json.loads(out)[0]["info"])[0][1] == pid
+        rc, out, _ = sdk_cmd.service_task_exec(config.SERVICE_NAME, "hello-0-server", "cat mount-data/marker")
+        assert rc == 0 and out.strip() == "kept"
+    finally:
+        sdk_install.uninstall(config.PACKAGE_NAME, config.SERVICE_NAME)
+
+
+def test_profile_mount_volume():
+    sdk_install.install(config.PACKAGE_NAME, config.SERVICE_NAME, 1,
+                        additional_options={"service": {"yaml": "profile-mount-volume"}})
+    try:
+        sdk_tasks.check_running(config.SERVICE_NAME, 1)
+        (path, _, size, source), = _volumes(_pod_info("hello-0")[0]["info"])
+        assert path == "fast-data" and size == 1000.0
+        assert source["profile"] == "fast-nvme" and source["mount"]["root"] == "/dcos/volume1"
+    finally:
+        sdk_install.uninstall(config.PACKAGE_NAME, config.SERVICE_NAME)

@@ -128,7 +128,7 @@ def test_multiport_and_overlay_ports():
         t = _launched(sim)["multiport-0-server"]
         env = {v.name: v.value for v in t.command.environment.variables}
         ports = {p.name: p.number for p in t.discovery.ports.ports}
-        assert ports["static"] == 5050 and ports["dynamic"] not in (0, 5050)
+        assert ports["static"] == 4444 and ports["dynamic"] not in (0, 4444)
         assert env["CUSTOM_ENV"] == str(ports["keyed"])  # only explicit env-keys become variables
         assert 7000 <= ports["ranged"] <= 7100
         vips = [lb.key for p in t.discovery.ports.ports for lb in p.labels.labels if lb.key.startswith("VIP_")]
