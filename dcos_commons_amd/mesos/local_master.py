@@ -469,20 +469,30 @@ class LocalMaster:
     def agent_resources(self, agent_id: str) -> List[P.Resource]:
         return self.call(lambda: self.agents[agent_id].available.to_resources())
 
+    def _held_resources(self, agent_id: str) -> List[P.Resource]:
+        """Everything an agent holds: available, offered, and used by executors and live tasks."""
+        a = self.agents[agent_id]
+        rs = a.available.to_resources()
+        for o in self.offers.values():
+            if o.agent_id == agent_id:
+                rs.extend(o.resources)
+        for e in a.executors.values():
+            rs.extend(e.resources)
+        for t in a.tasks.values():
+            if t.status.state not in TERMINAL:
+                rs.extend(t.resources)
+        return rs
+
     def reserved_resources(self, agent_id: str) -> List[P.Resource]:
         def do():
-            a = self.agents[agent_id]
-            rs = a.available.to_resources()
-            for o in self.offers.values():
-                if o.agent_id == agent_id:
-                    rs.extend(o.resources)
-            for e in a.executors.values():
-                rs.extend(e.resources)
-            for t in a.tasks.values():
-                if t.status.state not in TERMINAL:
-                    rs.extend(t.resources)
-            return [r for r in rs if len(r.reservations) and
+            return [r for r in self._held_resources(agent_id) if len(r.reservations) and
                     r.reservations[-1].type == P.Resource.ReservationInfo.DYNAMIC]
+        return self.call(do)
+
+    def persistent_volumes(self, agent_id: str) -> List[P.Resource]:
+        """Persistent volumes on an agent, whatever their reservation (static or dynamic)."""
+        def do():
+            return [r for r in self._held_resources(agent_id) if r.HasField("disk") and r.disk.persistence.id]
         return self.call(do)
 
     # -- framework-facing API (called through LocalSchedulerDriver) -------------------------
@@ -568,8 +578,18 @@ class LocalMaster:
             self._schedule(self.allocation_interval_s, self._periodic_allocate)
 
     def _offerable(self, fw: _Framework, r: P.Resource) -> bool:
-        role = effective_role(r)
-        return role == "*" or role in fw.roles
+        return self._alloc_role(fw, effective_role(r)) is not None
+
+    @staticmethod
+    def _alloc_role(fw: _Framework, role: str) -> Optional[str]:
+        """The framework role that may be allocated a resource reserved for ``role``: the role
+        itself, or (hierarchical roles) a sub-role of it, which can then refine the reservation
+        (``slave_public`` resources go to a framework subscribed as ``slave_public/<svc>-role``)."""
+        if role == "*":
+            return sorted(fw.roles)[0]
+        if role in fw.roles:
+            return role
+        return next((r for r in sorted(fw.roles) if r.startswith(role + "/")), None)
 
     def _allocate(self) -> None:
         now = self.clock()
@@ -592,10 +612,8 @@ class LocalMaster:
                     fw.filters.pop(a.id, None)
                 for r in mine:
                     a.available.subtract(r)
-                alloc_role = sorted(fw.roles)[0]
                 for r in mine:
-                    role = effective_role(r)
-                    r.allocation_info.role = role if role != "*" else alloc_role
+                    r.allocation_info.role = self._alloc_role(fw, effective_role(r))
                 oid = "offer-" + uuid.uuid4().hex
                 self.offers[oid] = _Offer(oid, fw.id, a.id, mine)
                 o = P.Offer(hostname=a.spec.hostname)

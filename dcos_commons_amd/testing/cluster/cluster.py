@@ -250,9 +250,13 @@ class LocalCluster:
             view.statuses.append(status)
 
     def frameworks(self, include_inactive: bool = False) -> List[dict]:
+        def multi(fw) -> bool:
+            return any(c.type == P.FrameworkInfo.Capability.MULTI_ROLE for c in fw.info.capabilities)
+
         def do():
             return [{"id": fid, "name": fw.info.name, "active": fw.connected, "roles": sorted(fw.roles),
-                     "webui_url": fw.info.webui_url}
+                     "webui_url": fw.info.webui_url,
+                     "role": None if multi(fw) else (fw.info.role or "*"), "multi_role": multi(fw)}
                     for fid, fw in self.master.frameworks.items() if include_inactive or fw.connected]
         return self.master.call(do)
 
@@ -270,6 +274,23 @@ class LocalCluster:
                 continue
             out.append(v)
         return sorted(out, key=lambda v: (v.name, v.statuses[0].timestamp if v.statuses else 0.0))
+
+    def task_roles(self, framework_name: str) -> Dict[str, str]:
+        """task name -> the role its resources are allocated to (``/mesos/state`` ``tasks[].role``):
+        the reservation role of its reserved resources."""
+        from dcos_commons_amd.mesos.resource_math import effective_role
+
+        def do():
+            out: Dict[str, str] = {}
+            for a in self.master.agents.values():
+                for t in a.tasks.values():
+                    fw = self.master.frameworks.get(t.framework_id)
+                    if fw is None or fw.info.name != framework_name or t.status.state in TERMINAL:
+                        continue
+                    roles = [effective_role(r) for r in t.info.resources]
+                    out[t.info.name] = next((r for r in roles if r != "*"), roles[0] if roles else "*")
+            return out
+        return self.master.call(do)
 
     def task(self, task_id: str) -> Optional[TaskView]:
         with self._tasks_lock:

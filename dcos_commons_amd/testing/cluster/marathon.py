@@ -29,7 +29,7 @@ import urllib.error
 import urllib.request
 import uuid
 from dataclasses import dataclass, field
-from typing import Dict, List, Optional
+from typing import Dict, List, Optional, Tuple
 
 LOGGER = logging.getLogger(__name__)
 REPO_ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
@@ -68,6 +68,9 @@ class MarathonTask:
                 "sandbox": self.sandbox}
 
 
+DEFAULT_APP_ROLE = "slave_public"
+
+
 @dataclass
 class _App:
     id: str
@@ -92,7 +95,46 @@ class LocalMarathon:
         self.restart_backoff_s = restart_backoff_s
         self.deploy_timeout_s = deploy_timeout_s
         self._apps: Dict[str, _App] = {}
+        self._groups: Dict[str, dict] = {}   # top-level group id -> definition ({"enforceRole": bool})
         self._lock = threading.Lock()
+
+    # -- groups and roles (Marathon 1.9 quota support) ---------------------------------------
+    def create_group(self, definition: dict) -> None:
+        gid = normalize_app_id(definition["id"])
+        with self._lock:
+            if gid in self._groups:
+                raise ValueError(f"Group {gid} is already created. Use PUT to change this group.")
+            self._groups[gid] = copy.deepcopy(definition)
+
+    def update_group(self, definition: dict) -> None:
+        gid = normalize_app_id(definition["id"])
+        with self._lock:
+            self._groups.setdefault(gid, {"id": gid}).update(copy.deepcopy(definition))
+
+    def delete_group(self, group_id: str) -> None:
+        gid = normalize_app_id(group_id)
+        for app_id in [a for a in self.app_ids() if a.startswith(gid + "/")]:
+            self.destroy_app(app_id)
+        with self._lock:
+            self._groups.pop(gid, None)
+
+    def groups(self) -> List[dict]:
+        with self._lock:
+            return [copy.deepcopy(g) for _, g in sorted(self._groups.items())]
+
+    def app_role(self, app_id: str, requested: Optional[str]) -> Tuple[str, bool]:
+        """(role, enforced) of an app: in a top-level group with ``enforceRole`` the group's name is
+        the only valid role; otherwise an app may ask for ``slave_public`` (the default) or its
+        top-level group's name, and any other role is reset to ``slave_public``."""
+        parts = normalize_app_id(app_id).strip("/").split("/")
+        group = "/" + parts[0] if len(parts) > 1 else None
+        with self._lock:
+            g = self._groups.get(group) if group else None
+        if g is not None and g.get("enforceRole"):
+            return parts[0], True
+        if requested and group is not None and requested == parts[0]:
+            return requested, False
+        return DEFAULT_APP_ROLE, False
 
     # -- queries ---------------------------------------------------------------------------
     def app_ids(self) -> List[str]:
@@ -291,7 +333,9 @@ class LocalMarathon:
             if isinstance(v, dict):  # {"secret": "..."} references
                 continue
             env[k] = str(v)
+        role, enforced = self.app_role(app.id, app.definition.get("role"))
         env.update({
+            "MESOS_ALLOCATION_ROLE": role, "MARATHON_APP_ENFORCE_GROUP_ROLE": "true" if enforced else "false",
             "PORT0": str(app.api_port), "PORT_API": str(app.api_port), "PORT": str(app.api_port),
             "PORTS": str(app.api_port), "MARATHON_APP_ID": app.id, "MARATHON_APP_VERSION": app.version,
             "MESOS_TASK_ID": task.id, "MESOS_SANDBOX": task.sandbox, "HOST": task.host,

@@ -129,9 +129,15 @@ def _state_summary() -> dict:
                "reserved_resources": by_agent.get(a["hostname"], {}),
                "domain": {"fault_domain": {"region": {"name": a["region"]}, "zone": {"name": a["zone"]}}},
                "attributes": a["attributes"]} for a in c.agents()]
-    frameworks = [{"id": f["id"], "name": f["name"], "active": f["active"], "roles": f["roles"],
-                   "webui_url": f.get("webui_url", "")}
-                  for f in c.frameworks()]
+    frameworks = []
+    for f in c.frameworks():
+        fw = {"id": f["id"], "name": f["name"], "active": f["active"], "webui_url": f.get("webui_url", "")}
+        if f.get("multi_role", True):
+            fw["roles"] = f["roles"]
+        else:
+            fw["role"] = f["role"]
+        fw["tasks"] = [{"name": n, "role": r} for n, r in sorted(c.task_roles(f["name"]).items())]
+        frameworks.append(fw)
     out = {"slaves": slaves, "frameworks": frameworks}
     if c.master.domain is not None:
         fd = c.master.domain.fault_domain
@@ -162,6 +168,24 @@ def cluster_request(method: str, cluster_path: str, retry: bool = True, raise_on
             body = c.dns_enumerate()
         elif path == "/dcos-metadata/dcos-version.json":
             body = {"version": c.dcos_version, "dcos-variant": "open"}
+        elif path.startswith("/marathon/v2/groups"):
+            gid = path[len("/marathon/v2/groups"):].split("?")[0]
+            if m == "GET":
+                body = {"groups": c.marathon.groups()}
+            elif m == "POST":
+                data, _ = _body(kwargs)
+                try:
+                    c.marathon.create_group(json.loads(data))
+                    body, status = {"deploymentId": "local"}, 201
+                except ValueError as e:
+                    body, status = {"message": str(e)}, 409
+            elif m == "PUT":
+                data, _ = _body(kwargs)
+                c.marathon.update_group(json.loads(data))
+                body = {"deploymentId": "local"}
+            elif m == "DELETE":
+                c.marathon.delete_group(gid)
+                body = {"deploymentId": "local"}
         elif path.startswith("/marathon/v2/apps"):
             app_id = path[len("/marathon/v2/apps"):].split("?")[0]
             if m == "GET" and not app_id.strip("/"):

@@ -80,3 +80,29 @@ def bump_task_count_config(service_name: str, key_name: str, delta: int = 1) -> 
     config["env"][key_name] = str(updated)
     update_app(config)
     return updated
+
+
+def create_group(group_id: str, options: Dict[str, Any]) -> None:
+    """``POST /v2/groups``: e.g. ``options={"enforceRole": True}`` makes the group's name the role
+    of every app under it (Marathon quota groups)."""
+    from dcos_commons_amd.testing.sdk import sdk_cmd
+
+    definition = dict(options)
+    definition["id"] = "/" + group_id.strip("/")
+    sdk_cmd.cluster_request("POST", "/marathon/v2/groups", json=definition, log_args=False, raise_on_error=False)
+
+
+def update_group(group_id: str, options: Dict[str, Any]) -> None:
+    from dcos_commons_amd.testing.sdk import sdk_cmd
+
+    definition = dict(options)
+    definition["id"] = "/" + group_id.strip("/")
+    sdk_cmd.cluster_request("PUT", "/marathon/v2/groups", json=definition, log_args=False, raise_on_error=False)
+
+
+def delete_group(group_id: str) -> None:
+    from dcos_commons_amd.testing.sdk import sdk_cmd
+
+    if group_id:   # an empty id would mean "/": every app of the cluster
+        sdk_cmd.cluster_request("DELETE", f"/marathon/v2/groups/{group_id.strip('/')}", log_args=False,
+                                raise_on_error=False)

@@ -57,8 +57,11 @@ def update_or_upgrade_or_downgrade(package_name: str, service_name: str, to_vers
     before = sdk_marathon.get_config(service_name).get("env", {})
     _update(package_name, service_name, to_version, to_options)
     after = sdk_marathon.get_config(service_name).get("env", {})
-    # package coordinates alone do not touch tasks; anything else in the scheduler env may
-    ignore = {"PACKAGE_VERSION", "PACKAGE_BUILD_TIME_EPOCH_MS", "PACKAGE_BUILD_TIME_STR"}
+    # package coordinates alone do not touch tasks, nor do role changes (quota migration moves a
+    # pod to the new role only when it is replaced: reference sdk_utils.filter_role_from_config);
+    # anything else in the scheduler env may
+    ignore = {"PACKAGE_VERSION", "PACKAGE_BUILD_TIME_EPOCH_MS", "PACKAGE_BUILD_TIME_STR",
+              "ENABLE_ROLE_MIGRATION", "MESOS_ALLOCATION_ROLE"}
     changed = {k for k in set(before) | set(after) if k not in ignore and before.get(k) != after.get(k)}
     if wait_for_deployment:
         if changed:

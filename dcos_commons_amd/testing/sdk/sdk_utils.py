@@ -133,8 +133,19 @@ def merge_dictionaries(dict1: Dict[str, Any], dict2: Dict[str, Any]) -> Dict[str
     return out
 
 
-def get_service_roles(service_name: str) -> List[str]:
-    return [get_role(service_name)]
+def get_service_roles(service_name: str) -> Dict[str, Any]:
+    """The service's roles as the master sees them: ``framework-roles`` (MULTI_ROLE frameworks) or
+    ``framework-role``, and ``task-roles`` (task name -> role of its resources)."""
+    from dcos_commons_amd.testing.sdk import sdk_cmd
+
+    state = sdk_cmd.cluster_request("GET", "/mesos/master/state").json()
+    out: Dict[str, Any] = {}
+    fw = next((f for f in state["frameworks"] if f["name"] == service_name and f["active"]), None)
+    if fw is not None:
+        out["framework-roles"] = fw.get("roles")
+        out["framework-role"] = fw.get("role") if "roles" not in fw else None
+        out["task-roles"] = {t["name"]: t["role"] for t in fw.get("tasks", [])}
+    return out
 
 
 def filter_role_from_config(config: Dict[str, Any]) -> Dict[str, Any]:
