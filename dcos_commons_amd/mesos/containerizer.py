@@ -104,8 +104,21 @@ def _cmdline(pid: int) -> str:
         return ""
 
 
+class SecretAccessDenied(Exception):
+    pass
+
+
+def secret_accessible(secret_path: str, space: str) -> bool:
+    """DC/OS secret spaces: a service at ``/a/b`` may read secrets stored directly under its own
+    path or any ancestor path (``a/b/x``, ``a/x``, ``x``), never deeper ones (``a/b/c/x``)."""
+    parent = [p for p in secret_path.strip("/").split("/")[:-1] if p]
+    own = [p for p in space.strip("/").split("/") if p]
+    return own[:len(parent)] == parent
+
+
 class ProcessTaskBehavior(TaskBehavior):
     executes_commands = True
+    _space: Optional[str] = None   # DCOS_SPACE of the task being launched (launches run on one thread)
 
     def __init__(self, work_dir: str, secret_resolver: Optional[Callable[[str], Optional[bytes]]] = None,
                  default_kill_grace_s: float = DEFAULT_KILL_GRACE_S, extra_env: Optional[Dict[str, str]] = None,
@@ -153,6 +166,7 @@ class ProcessTaskBehavior(TaskBehavior):
         with self._lock:
             self._procs[proc.task_id] = proc
         try:
+            self._space = self._dcos_space(master, task, agent)
             self._link_volumes(host, sandbox, list(info.resources) + self._executor_resources(master, task, agent))
             self._link_container_volumes(sandbox, info)
             self._fetch(sandbox, info.command.uris)
@@ -175,6 +189,15 @@ class ProcessTaskBehavior(TaskBehavior):
         threading.Thread(target=self._wait, args=(master, task, epoch, proc), name=f"wait-{info.name}",
                          daemon=True).start()
         master._schedule(0, master._lifecycle_starting, task, epoch, self.timing(info))
+
+    @staticmethod
+    def _dcos_space(master, task, agent) -> Optional[str]:
+        """The ``DCOS_SPACE`` label of the task's executor (the scheduler's Marathon app path),
+        which scopes the secrets the task may read; None when the executor carries none."""
+        e = agent.executors.get((task.framework_id, task.executor_id))
+        if e is None:
+            return None
+        return next((l.value for l in e.info.labels.labels if l.key == "DCOS_SPACE"), None)
 
     @staticmethod
     def _executor_resources(master, task, agent) -> List[P.Resource]:
@@ -222,7 +245,10 @@ class ProcessTaskBehavior(TaskBehavior):
             return secret.value.data
         if self.secret_resolver is None:
             return None
-        return self.secret_resolver(secret.reference.name)
+        name = secret.reference.name
+        if self._space is not None and not secret_accessible(name, self._space):
+            raise SecretAccessDenied(f"secret '{name}' is not accessible from DCOS_SPACE '{self._space}'")
+        return self.secret_resolver(name)
 
     def _fetch(self, sandbox: str, uris) -> None:
         for u in uris:

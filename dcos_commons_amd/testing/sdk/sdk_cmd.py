@@ -306,6 +306,32 @@ def run_cli(cmd: str, print_output: bool = True, check: bool = False) -> Tuple[i
     elif args[:3] == ["package", "repo", "list"]:
         rc, out, err = 0, json.dumps({"repositories": [{"name": r["name"], "uri": r["uri"]}
                                                        for r in c.cosmos.repositories]}) + "\n", ""
+    elif args[:2] == ["security", "secrets"] and len(args) >= 3:
+        # dcos security secrets create|update [--value=V | --text-file=F] <path> / delete <path> / list <dir>
+        sub = args[2]
+        pos = [a for a in args[3:] if not a.startswith("--")]
+        value = next((a.split("=", 1)[1] for a in args[3:] if a.startswith("--value=")), None)
+        text_file = next((a.split("=", 1)[1] for a in args[3:] if a.startswith("--text-file=")), None)
+        if text_file is not None:
+            with open(text_file, "rb") as f:
+                data = f.read()
+        else:
+            data = (value or "").encode("utf-8")
+        path = pos[0].strip("/") if pos else ""
+        if sub == "create" and path in c.secrets:
+            rc, out, err = 1, "", f"Secret '{path}' already exists\n"
+        elif sub in ("create", "update") and path:
+            if sub == "update" and path not in c.secrets:
+                rc, out, err = 1, "", f"Secret '{path}' not found\n"
+            else:
+                c.secrets[path] = data
+                rc, out, err = 0, "", ""
+        elif sub == "delete" and path:
+            rc, out, err = (0, "", "") if c.secrets.pop(path, None) is not None else \
+                (1, "", f"Secret '{path}' not found\n")
+        elif sub == "list":
+            prefix = (path + "/") if path else ""
+            rc, out, err = 0, "".join(f"- {k[len(prefix):]}\n" for k in sorted(c.secrets) if k.startswith(prefix)), ""
     elif args[:2] == ["task", "exec"]:
         rc, out, err = service_task_exec(None, args[2], " ".join(args[3:]))
     elif args[:2] == ["task", "ls"]:

@@ -17,7 +17,8 @@ ENV = dict(FRAMEWORK_NAME="hello-world", FRAMEWORK_PRINCIPAL="hello-world-princi
            HELLO_DISK="25", HELLO_GPUS="1", SLEEP_DURATION="1000", WORLD_COUNT="2",
            WORLD_PLACEMENT='[["hostname", "UNIQUE"]]', WORLD_CPUS="0.2", WORLD_MEM="512", WORLD_DISK="25",
            WORLD_READINESS_CHECK_INTERVAL="5", WORLD_READINESS_CHECK_DELAY="0", WORLD_READINESS_CHECK_TIMEOUT="10",
-           HELLO_VERSION="1", HELLO_SECRET1="hello-world/secret1", HELLO_SECRET2="hello-world/secret2",
+           HELLO_VERSION="1", HELLO_SECRET1="hello-world/secret1", HELLO_SECRET2="hello-world/secret2", WORLD_SECRET1="hello-world/secret1",
+           WORLD_SECRET2="hello-world/secret2", WORLD_SECRET3="hello-world/secret3",
            DISCOVERY_TASK_PREFIX="custom", GPU_PROBE_CMD="true", PRE_RESERVED_ROLE="slave_public",
            TASKCFG_ALL_GREETING="hi", TASKCFG_HELLO_TARGET="everyone")
 
