@@ -114,14 +114,15 @@ def test_container_features():
     _run("secrets.yml", secrets)
 
 
-def test_enable_disable_pod_section():
+def test_enable_disable_plan_steps():
     def without(sim):
-        assert not any(n.startswith("world-") for n in _launched(sim))
-    _run("enable-disable.yml", without)
+        assert not any(n.endswith("-server-a") for n in _launched(sim))
+        assert {"hello-0-server-b", "hello-1-server-b"} <= set(_launched(sim))
+    _run("enable-disable.yml", without, env={"TEST_BOOLEAN": "false"})
 
-    def with_world(sim):
-        assert {"world-0-server", "world-1-server"} <= set(_launched(sim))
-    _run("enable-disable.yml", with_world, env={"ENABLE_WORLD": "true"})
+    def with_a(sim):
+        assert {"hello-0-server-a", "hello-1-server-a", "hello-0-server-b"} <= set(_launched(sim))
+    _run("enable-disable.yml", with_a, env={"TEST_BOOLEAN": "true"})
 
 
 def test_multiport_and_overlay_ports():
