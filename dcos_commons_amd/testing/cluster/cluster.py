@@ -100,7 +100,7 @@ class LocalCluster:
                  agent_cpus: float = 8.0, agent_mem: float = 32768.0, agent_disk: float = 65536.0,
                  packages: Optional[Dict[str, str]] = None, scheduler_env: Optional[Dict[str, str]] = None,
                  finish_tasks: Sequence[str] = (), dcos_version: str = "1.13.0", keep_work_dir: bool = False,
-                 mount_disks: Sequence[tuple] = ()):
+                 mount_disks: Sequence[tuple] = (), dcos_security: bool = False):
         self.work_dir = os.path.abspath(work_dir or tempfile.mkdtemp(prefix="sdk-cluster-"))
         self._own_work_dir = work_dir is None and not keep_work_dir
         self.region = region
@@ -109,6 +109,13 @@ class LocalCluster:
         self.artifacts: Dict[str, str] = {}   # URI basename -> local file or extracted-archive directory
         self._stage_native_artifacts()
         self.secrets: Dict[str, bytes] = {}
+        # DC/OS Enterprise services (IAM login, secrets API, CA) for strict-mode scenarios: the
+        # schedulers' TLS artifacts and service-account logins go through them
+        self.dcos = None
+        if dcos_security:
+            from dcos_commons_amd.testing.dcos_fakes import FakeDcosCluster
+
+            self.dcos = FakeDcosCluster(require_auth=True, intermediate_ca=True, version=dcos_version)
         if executor == "process":
             from dcos_commons_amd.mesos.containerizer import ProcessTaskBehavior
 
@@ -121,7 +128,7 @@ class LocalCluster:
             task_env.update({k: v for k, v in os.environ.items()
                              if k.startswith(("HSA_", "ROCM_", "HIP_PLATFORM", "LD_LIBRARY_PATH"))})
             self.behavior = ProcessTaskBehavior(os.path.join(self.work_dir, "agents"),
-                                                secret_resolver=self.secrets.get, resolver=self.resolve,
+                                                secret_resolver=self.resolve_secret, resolver=self.resolve,
                                                 artifact_resolver=self.resolve_artifact, extra_env=task_env)
         elif executor == "synthetic":
             self.behavior = _SyntheticBehavior(finish_tasks)
@@ -153,6 +160,8 @@ class LocalCluster:
 
     # -- lifecycle -------------------------------------------------------------------------
     def start(self) -> "LocalCluster":
+        if self.dcos is not None:
+            self.dcos.start()
         self.zk = ZkServer().start()
         self.http_master = HttpMaster(self.master).start()
         for spec in self._agent_specs:
@@ -170,6 +179,8 @@ class LocalCluster:
         self.master.shutdown()
         if self.zk is not None:
             self.zk.stop()
+        if self.dcos is not None:
+            self.dcos.stop()
         if _current is self:
             use(None)
         if self._own_work_dir:
@@ -194,8 +205,30 @@ class LocalCluster:
             "SDK_ZK_SESSION_TIMEOUT_MS": "2000",
             "FRAMEWORK_LOG_LEVEL": "INFO",
         }
+        if self.dcos is not None:
+            env["SDK_DCOS_MASTER_URI"] = self.dcos.url
         env.update(self.extra_scheduler_env)
         return env
+
+    def resolve_secret(self, path: str) -> Optional[bytes]:
+        """The DC/OS secret store as Mesos' secret resolver sees it: secrets created through the
+        CLI, then (strict mode) those the schedulers wrote through the secrets API, e.g. TLS
+        artifacts; values of ``__dcos_base64__``-prefixed secrets are base64-decoded."""
+        path = path.strip("/")
+        if path in self.secrets:
+            return self.secrets[path]
+        if self.dcos is None:
+            return None
+        with self.dcos._lock:
+            entry = self.dcos.secrets.get(path)
+        if entry is None or "value" not in entry:
+            return None
+        value = entry["value"]
+        if os.path.basename(path).startswith("__dcos_base64__"):
+            import base64
+
+            return base64.b64decode(value)
+        return value.encode("utf-8") if isinstance(value, str) else value
 
     def _stage_native_artifacts(self) -> None:
         """``bootstrap.zip`` (every SDK task fetches it) holds this tree's native ``sdk-bootstrap``."""

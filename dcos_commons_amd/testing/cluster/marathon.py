@@ -329,8 +329,13 @@ class LocalMarathon:
     def _environment(self, app: _App, task: MarathonTask) -> Dict[str, str]:
         env = {k: os.environ[k] for k in ("PATH", "LANG", "LC_ALL", "TZ", "TMPDIR", "HOME") if k in os.environ}
         env.update(self.cluster.scheduler_environment())
+        secrets = app.definition.get("secrets") or {}
         for k, v in (app.definition.get("env") or {}).items():
-            if isinstance(v, dict):  # {"secret": "..."} references
+            if isinstance(v, dict):  # {"secret": "<name>"} -> app "secrets": {"<name>": {"source": path}}
+                source = (secrets.get(v.get("secret", "")) or {}).get("source")
+                data = self.cluster.resolve_secret(source) if source else None
+                if data is not None:
+                    env[k] = data.decode("utf-8", "replace")
                 continue
             env[k] = str(v)
         role, enforced = self.app_role(app.id, app.definition.get("role"))
