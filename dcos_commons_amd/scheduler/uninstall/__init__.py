@@ -130,6 +130,16 @@ def get_resource_ids_by_agent_host(state_store) -> Dict[str, Set[str]]:
     return dict(sorted(out.items()))
 
 
+def _has_tls_artifacts(secrets_client, secrets_namespace: str) -> bool:
+    from dcos_commons_amd.offer.evaluate.security import known_tls_artifacts
+
+    try:
+        return bool(known_tls_artifacts(secrets_client.list(secrets_namespace)))
+    except Exception:  # noqa: BLE001 -- the store is unreachable: keep the reference's spec-only rule
+        LOGGER.warning("Could not list the secret store: TLS artifacts of earlier configs may stay behind")
+        return False
+
+
 class UninstallPlanFactory:
     def __init__(self, service_spec, state_store, scheduler_config, namespace: Optional[str] = None,
                  secrets_client=None):
@@ -141,10 +151,13 @@ class UninstallPlanFactory:
             steps = [ResourceCleanupStep(rid, namespace) for rid in sorted(ids)]
             self.resource_cleanup_steps.extend(steps)
             phases.append(DefaultPhase(RESOURCE_PHASE_PREFIX + host, list(steps), ParallelStrategy(), []))
-        if has_tasks_with_tls(service_spec) and secrets_client is not None:
-            phases.append(DefaultPhase(TLS_CLEANUP_PHASE, [TLSCleanupStep(
-                secrets_client, scheduler_config.secrets_namespace(service_spec.name), namespace)],
-                SerialStrategy(), []))
+        secrets_ns = scheduler_config.secrets_namespace(service_spec.name)
+        if secrets_client is not None and (has_tasks_with_tls(service_spec)
+                                           or _has_tls_artifacts(secrets_client, secrets_ns)):
+            # Unlike the reference (UninstallPlanFactory.java:110-115), artifacts left by an earlier
+            # configuration that had TLS turned on are found too: the secret store is listed.
+            phases.append(DefaultPhase(TLS_CLEANUP_PHASE, [TLSCleanupStep(secrets_client, secrets_ns, namespace)],
+                                       SerialStrategy(), []))
         self.deregister_step = DeregisterStep(namespace)
         dereg = DefaultPhase(DEREGISTER_PHASE, [self.deregister_step], SerialStrategy(), [])
         helper = DependencyStrategyHelper(phases)
@@ -237,8 +250,10 @@ class UninstallScheduler:
             self.logger.info("Service has been told to uninstall. Marking this in the persistent state store. "
                              "Uninstall cannot be canceled once triggered.")
             state_store_utils.set_uninstalling(state_store)
-        if secrets_client is None and has_tasks_with_tls(service_spec):
+        has_account = bool(scheduler_config.env.get_optional("DCOS_SERVICE_ACCOUNT_CREDENTIAL", None))
+        if secrets_client is None and (has_tasks_with_tls(service_spec) or has_account):
             # UninstallScheduler.java:90-105: TLS secrets are cleaned up with the service account's token
+            # (with an account but no TLS in the current spec: artifacts of earlier TLS configs)
             try:
                 from dcos_commons_amd.dcos.clients import DcosHttpExecutor, SecretsClient
 

@@ -828,6 +828,12 @@ class ServiceTestRunner:
             for task in pod.tasks:
                 env = get_task_environment(spec.name, pi, task, cfg)
                 env.update(DCOS_TASK_ENVVARS)
+                # a pod whose placement names zones/regions only launches on offers that carry a
+                # fault domain, so its tasks always see ZONE/REGION (PodInfoBuilder adds them)
+                if env.get("PLACEMENT_REFERENCED_ZONE") == "true":
+                    env.setdefault("ZONE", "test-zone")
+                if env.get("PLACEMENT_REFERENCED_REGION") == "true":
+                    env.setdefault("REGION", "test-region")
                 for r in task.resource_set.resources:
                     if isinstance(r, PortSpec) and r.env_key:
                         env[r.env_key] = str(r.port or rng.randrange(32768, 61000))
