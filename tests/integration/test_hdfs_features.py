@@ -1,0 +1,97 @@
+"""HDFS features on a strict-mode local cluster (synthetic task payloads).
+
+Reference: frameworks/hdfs/tests/{test_overlay.py, test_tls.py, test_racks.py, test_upgrade.py}.
+Every node type joins the overlay network (container addresses, no host ports) while the
+``hdfs-site.xml`` / ``core-site.xml`` endpoints keep being served; with transport encryption each
+journal, name and data node gets keystore artifacts from the cluster CA and ``hdfs-site.xml``
+switches to ``HTTPS_ONLY`` with the HTTPS addresses; zone placement makes data nodes rack-aware
+(each sees its zone); the package upgrades to the newest published version and back.
+"""
+import pytest
+
+from dcos_commons_amd.testing.sdk import (sdk_agents, sdk_cmd, sdk_install, sdk_networks, sdk_plan, sdk_security,
+                                          sdk_tasks, sdk_upgrade)
+from tests.integration.conftest import make_cluster
+from tests.integration.test_hdfs import DEFAULT_TASK_COUNT, FINISH_TASKS, PACKAGE
+
+SVC = "hdfs"
+ACCOUNT, ACCOUNT_SECRET = "hdfs-principal", "hdfs-secret"
+
+
+@pytest.fixture(scope="module")
+def local_cluster():
+    c = make_cluster(executor="synthetic", finish_tasks=FINISH_TASKS, dcos_security=True)
+    sdk_security.create_service_account(ACCOUNT, ACCOUNT_SECRET)
+    yield c
+    c.shutdown()
+
+
+pytestmark = pytest.mark.usefixtures("local_cluster")
+
+
+def _info(task):
+    pod = task.rsplit("-", 1)[0]
+    return next(t["info"] for t in sdk_cmd.service_request("GET", SVC, f"/v1/pod/{pod}/info").json()
+                if t["info"]["name"] == task)
+
+
+def test_tasks_and_endpoints_on_overlay():
+    sdk_install.install(PACKAGE, SVC, DEFAULT_TASK_COUNT, additional_options=sdk_networks.ENABLE_VIRTUAL_NETWORKS_OPTIONS)
+    try:
+        tasks = sdk_tasks.get_service_tasks(SVC)
+        assert len(tasks) == DEFAULT_TASK_COUNT
+        for t in tasks:
+            sdk_networks.check_task_network(t.name)
+            assert sdk_networks.get_task_ip(SVC, t.name).startswith("9."), t.name
+            assert "ports" not in t.resources, t.name
+        assert set(sdk_networks.get_endpoint_names(PACKAGE, SVC)) >= {"hdfs-site.xml", "core-site.xml"}
+        assert "dfs.namenode.rpc-address" in sdk_networks.get_endpoint_string(PACKAGE, SVC, "hdfs-site.xml")
+    finally:
+        sdk_install.uninstall(PACKAGE, SVC)
+
+
+def test_transport_encryption():
+    sdk_install.install(PACKAGE, SVC, DEFAULT_TASK_COUNT, additional_options={
+        "service": {"service_account": ACCOUNT, "service_account_secret": ACCOUNT_SECRET,
+                    "security": {"transport_encryption": {"enabled": True}}}})
+    try:
+        site = sdk_networks.get_endpoint_string(PACKAGE, SVC, "hdfs-site.xml")
+        assert "HTTPS_ONLY" in site and "dfs.namenode.https-address" in site
+        for task in ("journal-0-node", "name-0-node", "name-1-node", "data-0-node"):
+            vols = [v["containerPath"] for v in _info(task).get("container", {}).get("volumes", [])
+                    if v.get("source", {}).get("type") == "SECRET"]
+            assert any(v.endswith(".keystore") for v in vols) and any(v.endswith(".truststore") for v in vols), \
+                (task, vols)
+        # one signed certificate per TLS-enabled task, stored under the service's secret namespace
+        names = sdk_security.list_secrets(SVC)
+        assert sum(1 for n in names if n.endswith("keystore")) >= 6, names
+        assert len(sdk_install._cluster().dcos.signed) >= 6
+    finally:
+        sdk_install.uninstall(PACKAGE, SVC)
+    assert not [n for n in sdk_security.list_secrets(SVC) if n.endswith(("keystore", "truststore"))]
+
+
+def test_detect_racks():
+    sdk_install.install(PACKAGE, SVC, DEFAULT_TASK_COUNT, additional_options={
+        "data_node": {"placement_constraint": '[["@zone", "GROUP_BY", "3"]]'}})
+    try:
+        zones = {a["hostname"]: a["zone"] for a in sdk_agents.get_agents()}
+        data = [t for t in sdk_tasks.get_service_tasks(SVC) if t.name.startswith("data-")]
+        assert len(data) == 3
+        assert len({zones[t.host] for t in data}) == 3                 # spread over the 3 zones
+        for t in data:
+            env = {v["name"]: v.get("value") for v in _info(t.name)["command"]["environment"]["variables"]}
+            assert env["PLACEMENT_REFERENCED_ZONE"] == "true" and env["ZONE"] == zones[t.host]
+    finally:
+        sdk_install.uninstall(PACKAGE, SVC)
+
+
+def test_upgrade_and_downgrade():
+    sdk_upgrade.test_upgrade(PACKAGE, SVC, DEFAULT_TASK_COUNT)
+    try:
+        sdk_plan.wait_for_completed_deployment(SVC)
+        sdk_tasks.check_running(SVC, DEFAULT_TASK_COUNT)
+        sdk_upgrade.test_downgrade(PACKAGE, SVC, DEFAULT_TASK_COUNT)
+        sdk_plan.wait_for_completed_deployment(SVC)
+    finally:
+        sdk_install.uninstall(PACKAGE, SVC)
