@@ -155,6 +155,9 @@ class LocalCluster:
         self.zk: Optional[ZkServer] = None
         self.http_master: Optional[HttpMaster] = None
         self.marathon = LocalMarathon(self)
+        from dcos_commons_amd.testing.cluster.metronome import LocalMetronome
+
+        self.metronome = LocalMetronome(self)
         self.cosmos = LocalCosmos(self, packages)
         self._started = False
 
@@ -174,6 +177,7 @@ class LocalCluster:
             return
         self._started = False
         self.marathon.shutdown()
+        self.metronome.shutdown()
         if self.http_master is not None:
             self.http_master.stop()
         self.master.shutdown()
