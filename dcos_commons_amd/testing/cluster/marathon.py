@@ -404,7 +404,12 @@ class LocalMarathon:
 
     def _supervise(self, app: _App) -> None:
         while not app.destroyed:
-            self._start(app)
+            try:
+                self._start(app)
+            except RuntimeError as e:   # no agent satisfies the app's constraints (yet): stay waiting
+                LOGGER.warning("Marathon: cannot place %s: %s", app.id, e)
+                time.sleep(self.restart_backoff_s)
+                continue
             proc = app.proc
             while proc.poll() is None:
                 # only the process started for the current version completes a deployment (the
