@@ -70,3 +70,37 @@ def test_upgrade_to_an_airgap_bundle(built):
 def test_uninstall_packaged_service(built):
     sdk_install.uninstall(config.PACKAGE_NAME, SVC)
     assert not sdk_marathon.app_exists(SVC)
+
+
+@pytest.mark.parametrize("store", ["aws", "azure"])
+def test_install_from_object_store(built, store, tmp_path, monkeypatch):
+    """tools/publish_aws.py / publish_azure.py: artifacts and the stub universe go to a bucket
+    (container) under a unique directory; the repo URL is the bucket's HTTP address."""
+    from dcos_commons_amd.tools.publish_object_store import aws_publisher, azure_publisher
+    from dcos_commons_amd.tools.universe.uploaders import LocalObjectStore
+
+    c, _, artifacts, _ = built
+    monkeypatch.setenv("SDK_OBJECT_STORE_ROOT", str(tmp_path / "store"))
+    monkeypatch.setenv("UNIVERSE_URL_PATH", str(tmp_path / "url.txt"))
+    version = f"3.0.0-{store}"
+    make = aws_publisher if store == "aws" else azure_publisher
+    url = make(config.PACKAGE_NAME, version, os.path.join(HELLO_DIR, "universe"), artifacts).upload(str(tmp_path / "w"))
+    try:
+        assert open(tmp_path / "url.txt").read().strip() == url
+        assert ("/infinity-artifacts/autodelete7d/" if store == "aws" else "/infinityartifacts/artifacts/") in url
+        bucket_dir = os.path.dirname(url.split("/", 3)[3])
+        for a in artifacts:   # every artifact landed next to the stub universe
+            assert os.path.exists(os.path.join(str(tmp_path / "store"), bucket_dir, os.path.basename(a)))
+        rc, out, _ = sdk_cmd.run_cli(f"package repo add {store}-repo {url}")
+        assert rc == 0 and f"hello-world {version}" in out
+        svc = f"{SVC}-{store}"
+        sdk_install.install(config.PACKAGE_NAME, svc, config.DEFAULT_TASK_COUNT, package_version=version)
+        try:
+            env = sdk_marathon.get_config(svc)["env"]
+            assert env["PACKAGE_VERSION"] == version and env["BOOTSTRAP_URI"].startswith(url.rsplit("/", 1)[0])
+            sdk_plan.wait_for_completed_deployment(svc)
+        finally:
+            sdk_install.uninstall(config.PACKAGE_NAME, svc)
+        sdk_cmd.run_cli(f"package repo remove {store}-repo")
+    finally:
+        LocalObjectStore.get(str(tmp_path / "store")).stop()
