@@ -222,3 +222,44 @@ def test_scheduler_zip_launcher_runs_from_the_unpacked_artifact(tmp_path):
     assert out.returncode == 0, out.stderr
     lib, specs = out.stdout.split()
     assert lib.startswith(str(tmp_path / "x")) and specs == str(tmp_path / "x" / "hello-world-scheduler" / "specs")
+
+
+def test_print_package_tag_version_and_sha(tmp_path, capsys):
+    """tools/print_package_tag.py: the described version, then the SHA it is tagged at in a
+    local checkout and through ``git ls-remote``."""
+    import subprocess
+
+    from dcos_commons_amd.tools import print_package_tag as ppt
+
+    repo = tmp_path / "repo"
+    repo.mkdir()
+    git = ["git", "-C", str(repo), "-c", "user.email=ci@example.com", "-c", "user.name=ci"]
+    subprocess.run(["git", "init", "-q", str(repo)], check=True)
+    (repo / "f").write_text("x")
+    subprocess.run(git + ["add", "f"], check=True)
+    subprocess.run(git + ["commit", "-qm", "c"], check=True)
+    subprocess.run(git + ["tag", "-a", "2.3.0-1.0", "-m", "release"], check=True)
+    sha = subprocess.check_output(["git", "-C", str(repo), "rev-parse", "HEAD"]).decode().strip()
+
+    def describe(name):
+        return {"version": "2.3.0-1.0"}
+    assert ppt.main(["ppt", "hello-world"], describe) == 0
+    assert capsys.readouterr().out.strip() == "2.3.0-1.0"
+    assert ppt.main(["ppt", "hello-world", str(repo)], describe) == 0
+    assert capsys.readouterr().out.strip() == sha
+    assert ppt.PackageVersion("hello-world", describe).get_version_sha_for_url(str(repo)) == sha
+    assert ppt.main(["ppt"], describe) == 1
+
+
+def test_save_properties_uploads_to_the_object_store(tmp_path, monkeypatch):
+    from dcos_commons_amd.tools import save_properties
+
+    monkeypatch.setenv("WORKSPACE", str(tmp_path))
+    monkeypatch.setenv("SDK_OBJECT_STORE_ROOT", str(tmp_path / "store"))
+    (tmp_path / "stub-universe.properties").write_text("STUB_UNIVERSE_URL=http://x/stub.json\n")
+    assert save_properties.main(["save", "s3://bucket/ci/run-1"]) == 0
+    assert (tmp_path / "store" / "bucket" / "ci" / "run-1" / "stub-universe.properties").read_text() == \
+        "STUB_UNIVERSE_URL=http://x/stub.json\n"
+    monkeypatch.setenv("WORKSPACE", str(tmp_path / "missing"))
+    with pytest.raises(FileNotFoundError):
+        save_properties.upload_to_s3("s3://bucket/ci")
