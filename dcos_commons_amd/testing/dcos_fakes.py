@@ -35,6 +35,9 @@ class FakeDcosCluster:
         self.version = version
         self.secrets: Dict[str, dict] = {}
         self.service_accounts: Dict[str, str] = {}  # uid -> public key PEM
+        self.users: Dict[str, str] = {}             # uid -> password
+        self.cluster_id = "local-" + "%08x" % (id(self) & 0xffffffff)
+        self.cluster_name = "local-dcos"
         self.issued: Dict[str, float] = {}
         self.logins = 0
         self.signed: List[str] = []
@@ -80,8 +83,21 @@ class FakeDcosCluster:
                            "login_endpoint": self.url + "/acs/api/v1/auth/login"})
 
     # -- handlers -------------------------------------------------------------------------
+    def add_user(self, uid: str, password: str) -> None:
+        """A local user account (``dcos auth login --username/--password``)."""
+        self.users[uid] = password
+
     def login(self, body: dict):
         uid, token = body.get("uid"), body.get("token")
+        if uid in self.users and "password" in body:
+            if body["password"] != self.users[uid]:
+                return 401, {"title": "Invalid authentication credentials"}
+            exp = int(time.time() + self.token_lifetime_s)
+            session = native().jwt_rs256(self._iam_key, {"uid": uid, "exp": exp})
+            with self._lock:
+                self.issued[session] = exp
+                self.logins += 1
+            return 200, {"token": session}
         pub = self.service_accounts.get(uid)
         claims = native().verify_jwt(pub, token) if pub and token else None
         if claims is None or claims.get("uid") != uid or claims.get("exp", 0) < time.time():
@@ -182,7 +198,11 @@ class _Handler(BaseHTTPRequestHandler):
         if not c.authorized(self.headers.get("Authorization")):
             self._reply(401, {"title": "Unauthorized"})
             return
-        if u.path == "/ca/api/v2/sign" and method == "POST":
+        if u.path == "/metadata" and method == "GET":
+            self._reply(200, {"CLUSTER_ID": c.cluster_id, "PUBLIC_IPV4": "127.0.0.1"})
+        elif u.path == "/mesos/state-summary" and method == "GET":
+            self._reply(200, {"cluster": c.cluster_name, "slaves": [], "frameworks": []})
+        elif u.path == "/ca/api/v2/sign" and method == "POST":
             self._reply(*c.sign(body or {}))
         elif u.path == "/ca/api/v2/bundle" and method == "POST":
             self._reply(*c.bundle(body or {}))

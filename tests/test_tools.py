@@ -263,3 +263,29 @@ def test_save_properties_uploads_to_the_object_store(tmp_path, monkeypatch):
     monkeypatch.setenv("WORKSPACE", str(tmp_path / "missing"))
     with pytest.raises(FileNotFoundError):
         save_properties.upload_to_s3("s3://bucket/ci")
+
+
+@needs_native
+def test_dcos_login_user_and_service_account(tmp_path, monkeypatch):
+    """tools/dcos_login.py against the fake IAM: user/password and service-account logins, the
+    attached cluster config carries a token the cluster accepts."""
+    from dcos_commons_amd.testing.dcos_fakes import FakeDcosCluster
+    from dcos_commons_amd.tools import dcos_login
+
+    cluster = FakeDcosCluster().start()
+    try:
+        cluster.add_user("bootstrapuser", "deleteme")
+        monkeypatch.setenv("CLUSTER_URL", cluster.url)
+        monkeypatch.setenv("DCOS_DIR", str(tmp_path / "dcos"))
+        path = dcos_login.login_session()
+        text = open(path).read()
+        token = text.split('dcos_acs_token = "')[1].split('"')[0]
+        assert cluster.authorized(f"token={token}") and f'dcos_url = "{cluster.url}"' in text
+        assert os.path.exists(os.path.join(os.path.dirname(path), "attached"))
+        with pytest.raises(Exception):
+            dcos_login.login(cluster.url, "bootstrapuser", "wrong")
+        cred = cluster.add_service_account("ci-account")
+        token = dcos_login.login(cluster.url, service_account_credential=cred)
+        assert cluster.authorized(f"token={token}")
+    finally:
+        cluster.stop()
