@@ -356,6 +356,19 @@ class LocalMaster:
             return aid
         return self.call(do)
 
+    def add_mount_disks(self, agent_id: str, disks) -> None:
+        """Attach MOUNT disks (``(root, size[, profile])``) to a registered agent, as an agent
+        restarted with new ``--resources`` re-registers with them; its tasks keep running."""
+        def do():
+            a = self.agents[agent_id]
+            extra = AgentSpec(hostname=a.spec.hostname, cpus=0, mem=0, disk=0, ports=(),
+                              mount_disks=tuple(disks)).resources()
+            for r in extra:
+                a.available.add(r)
+            a.spec.mount_disks = tuple(a.spec.mount_disks) + tuple(disks)
+            self._allocate()
+        self.call(do)
+
     def lose_agent(self, agent_id: str, partition_aware: bool = True) -> None:
         """Agent disappears: outstanding offers are rescinded and its tasks go UNREACHABLE/LOST."""
         def do():

@@ -408,6 +408,22 @@ class LocalCluster:
         """The operator marks the agent GONE (``dcos node decommission``)."""
         self.master.gone_by_operator(self._agent(host))
 
+    def create_testing_volumes(self, count: int = 2, size_mb: float = 10240.0, profile: Optional[str] = None,
+                               hosts: Optional[Sequence[str]] = None) -> List[str]:
+        """``/dcos/volume<i>`` MOUNT disks on every agent (or on ``hosts``), numbered after the
+        ones the agent already has (reference tools/create_testing_volumes.py); returns the roots."""
+        roots: List[str] = []
+        for host, aid in sorted(self.agent_ids.items()):
+            if hosts is not None and host not in hosts:
+                continue
+            spec = self.master.agents[aid].spec
+            start = len(spec.mount_disks)
+            disks = [(f"/dcos/volume{start + i}", float(size_mb)) + ((profile,) if profile else ())
+                     for i in range(count)]
+            self.master.add_mount_disks(aid, disks)
+            roots.extend(d[0] for d in disks)
+        return roots
+
     def add_agent(self, spec: AgentSpec) -> str:
         aid = self.master.add_agent(spec)
         self.agent_ids[spec.hostname] = aid

@@ -143,3 +143,24 @@ def test_profile_mount_volume():
         assert source["profile"] == "fast-nvme" and source["mount"]["root"] == "/dcos/volume1"
     finally:
         sdk_install.uninstall(config.PACKAGE_NAME, config.SERVICE_NAME)
+
+
+def test_testing_volumes_added_to_running_agents(local_cluster):
+    """tools/create_testing_volumes.py: agents re-register with new /dcos/volume<N> disks and a
+    profiled MOUNT volume deploys onto them without disturbing anything running."""
+    from dcos_commons_amd.tools.create_testing_volumes import create_testing_volumes
+
+    roots = create_testing_volumes(local_cluster, count=1, size_mb=300.0, profile="xfs")
+    assert roots and all(r == "/dcos/volume2" for r in roots)   # after the module's two disks
+    for aid in local_cluster.agent_ids.values():
+        offered = [r for r in local_cluster.master.agent_resources(aid)
+                   if r.HasField("disk") and r.disk.source.mount.root == "/dcos/volume2"]
+        assert len(offered) == 1 and offered[0].disk.source.profile == "xfs" and offered[0].scalar.value == 300.0
+    sdk_install.install(config.PACKAGE_NAME, config.SERVICE_NAME, 1, additional_options={
+        "service": {"yaml": "profile-mount-volume"}})
+    try:
+        (path, _, size, source), = _volumes(_pod_info("hello-0")[0]["info"])
+        # 500 MB asked, but only the 1 GB fast-nvme disks carry that profile: the xfs disks are ignored
+        assert source["profile"] == "fast-nvme"
+    finally:
+        sdk_install.uninstall(config.PACKAGE_NAME, config.SERVICE_NAME)
