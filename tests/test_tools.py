@@ -289,3 +289,21 @@ def test_dcos_login_user_and_service_account(tmp_path, monkeypatch):
         assert cluster.authorized(f"token={token}")
     finally:
         cluster.stop()
+
+
+def test_validate_pip_freeze():
+    from dcos_commons_amd.tools import validate_pip_freeze as v
+
+    installed = {"pyyaml": "6.0.1", "requests": "2.31.0", "sdk-testing": "0.1"}
+    good = "PyYAML==6.0.1\n# comment\nrequests==2.31.0  # pinned\n" \
+           "git+https://github.com/acme/sdk-testing.git@abc#egg=x&validator-hint: name=sdk-testing version=SNAPSHOT\n"
+    assert v.validate(good, installed) == []
+    bad = "PyYAML>=6\nrequests==2.30.0\nsdk-testing==0.1\nsdk_testing==0.1\nmissing==1.0\n"
+    problems = v.validate(bad, installed)
+    assert any("not pinned" in p for p in problems) and any("duplicate" in p for p in problems)
+    assert any("missing==1.0 is not installed" in p for p in problems)
+    assert any("requests: requirements pin" in p for p in problems)
+    # this interpreter's own packages validate against themselves
+    import yaml
+
+    assert v.validate(f"PyYAML=={yaml.__version__}\n") == []
