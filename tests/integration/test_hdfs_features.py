@@ -16,6 +16,14 @@ from tests.integration.test_hdfs import DEFAULT_TASK_COUNT, FINISH_TASKS, PACKAG
 
 SVC = "hdfs"
 ACCOUNT, ACCOUNT_SECRET = "hdfs-principal", "hdfs-secret"
+# data nodes pass their first readiness check after 1 s instead of the default 10 s
+FAST = {"data_node": {"readiness_check": {"delay": 1, "interval": 1}}}
+
+
+def _opts(extra):
+    from dcos_commons_amd.testing.sdk.sdk_utils import merge_dictionaries
+
+    return merge_dictionaries(FAST, extra)
 
 
 @pytest.fixture(scope="module")
@@ -36,7 +44,8 @@ def _info(task):
 
 
 def test_tasks_and_endpoints_on_overlay():
-    sdk_install.install(PACKAGE, SVC, DEFAULT_TASK_COUNT, additional_options=sdk_networks.ENABLE_VIRTUAL_NETWORKS_OPTIONS)
+    sdk_install.install(PACKAGE, SVC, DEFAULT_TASK_COUNT,
+                        additional_options=_opts(sdk_networks.ENABLE_VIRTUAL_NETWORKS_OPTIONS))
     try:
         tasks = sdk_tasks.get_service_tasks(SVC)
         assert len(tasks) == DEFAULT_TASK_COUNT
@@ -51,9 +60,9 @@ def test_tasks_and_endpoints_on_overlay():
 
 
 def test_transport_encryption():
-    sdk_install.install(PACKAGE, SVC, DEFAULT_TASK_COUNT, additional_options={
+    sdk_install.install(PACKAGE, SVC, DEFAULT_TASK_COUNT, additional_options=_opts({
         "service": {"service_account": ACCOUNT, "service_account_secret": ACCOUNT_SECRET,
-                    "security": {"transport_encryption": {"enabled": True}}}})
+                    "security": {"transport_encryption": {"enabled": True}}}}))
     try:
         site = sdk_networks.get_endpoint_string(PACKAGE, SVC, "hdfs-site.xml")
         assert "HTTPS_ONLY" in site and "dfs.namenode.https-address" in site
@@ -72,8 +81,8 @@ def test_transport_encryption():
 
 
 def test_detect_racks():
-    sdk_install.install(PACKAGE, SVC, DEFAULT_TASK_COUNT, additional_options={
-        "data_node": {"placement_constraint": '[["@zone", "GROUP_BY", "3"]]'}})
+    sdk_install.install(PACKAGE, SVC, DEFAULT_TASK_COUNT, additional_options=_opts({
+        "data_node": {"placement_constraint": '[["@zone", "GROUP_BY", "3"]]'}}))
     try:
         zones = {a["hostname"]: a["zone"] for a in sdk_agents.get_agents()}
         data = [t for t in sdk_tasks.get_service_tasks(SVC) if t.name.startswith("data-")]
@@ -87,7 +96,7 @@ def test_detect_racks():
 
 
 def test_upgrade_and_downgrade():
-    sdk_upgrade.test_upgrade(PACKAGE, SVC, DEFAULT_TASK_COUNT)
+    sdk_upgrade.test_upgrade(PACKAGE, SVC, DEFAULT_TASK_COUNT, from_options=FAST, to_options=FAST)
     try:
         sdk_plan.wait_for_completed_deployment(SVC)
         sdk_tasks.check_running(SVC, DEFAULT_TASK_COUNT)
