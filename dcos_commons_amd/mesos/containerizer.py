@@ -118,7 +118,6 @@ def secret_accessible(secret_path: str, space: str) -> bool:
 
 class ProcessTaskBehavior(TaskBehavior):
     executes_commands = True
-    _space: Optional[str] = None   # DCOS_SPACE of the task being launched (launches run on one thread)
 
     def __init__(self, work_dir: str, secret_resolver: Optional[Callable[[str], Optional[bytes]]] = None,
                  default_kill_grace_s: float = DEFAULT_KILL_GRACE_S, extra_env: Optional[Dict[str, str]] = None,
@@ -166,11 +165,11 @@ class ProcessTaskBehavior(TaskBehavior):
         with self._lock:
             self._procs[proc.task_id] = proc
         try:
-            self._space = self._dcos_space(master, task, agent)
+            space = self._dcos_space(master, task, agent)
             self._link_volumes(host, sandbox, list(info.resources) + self._executor_resources(master, task, agent))
-            self._link_container_volumes(sandbox, info)
+            self._link_container_volumes(sandbox, info, space)
             self._fetch(sandbox, info.command.uris)
-            proc.env = self._environment(master, task, agent, sandbox)
+            proc.env = self._environment(master, task, agent, sandbox, space)
             with open(os.path.join(sandbox, "stdout"), "ab") as out, open(os.path.join(sandbox, "stderr"), "ab") as err:
                 # the task's shell is named like the executor that would run it on Mesos, so a
                 # `pkill -f mesos-default-executor` takes the task down with "its executor"
@@ -224,11 +223,11 @@ class ProcessTaskBehavior(TaskBehavior):
             os.makedirs(target, exist_ok=True)
             self._link(target, sandbox, r.disk.volume.container_path)
 
-    def _link_container_volumes(self, sandbox: str, info: P.TaskInfo) -> None:
+    def _link_container_volumes(self, sandbox: str, info: P.TaskInfo, space: Optional[str] = None) -> None:
         for v in info.container.volumes:
             src = v.source
             if src.type == P.Volume.Source.SECRET:
-                data = self._secret(src.secret)
+                data = self._secret(src.secret, space)
                 path = os.path.join(sandbox, v.container_path)
                 os.makedirs(os.path.dirname(path), exist_ok=True)
                 with open(path, "wb") as f:
@@ -240,14 +239,15 @@ class ProcessTaskBehavior(TaskBehavior):
                 os.makedirs(target, exist_ok=True)
                 self._link(target, sandbox, v.container_path)
 
-    def _secret(self, secret: P.Secret) -> Optional[bytes]:
+    def _secret(self, secret: P.Secret, space: Optional[str] = None) -> Optional[bytes]:
+        """The secret's bytes; a reference outside ``space`` (the task's DCOS_SPACE) is refused."""
         if secret.type == P.Secret.VALUE:
             return secret.value.data
         if self.secret_resolver is None:
             return None
         name = secret.reference.name
-        if self._space is not None and not secret_accessible(name, self._space):
-            raise SecretAccessDenied(f"secret '{name}' is not accessible from DCOS_SPACE '{self._space}'")
+        if space is not None and not secret_accessible(name, space):
+            raise SecretAccessDenied(f"secret '{name}' is not accessible from DCOS_SPACE '{space}'")
         return self.secret_resolver(name)
 
     def _fetch(self, sandbox: str, uris) -> None:
@@ -289,12 +289,12 @@ class ProcessTaskBehavior(TaskBehavior):
                 except (shutil.ReadError, ValueError, OSError) as e:
                     LOGGER.warning("fetcher: cannot extract %s: %s", dest, e)
 
-    def _environment(self, master, task, agent, sandbox: str) -> Dict[str, str]:
+    def _environment(self, master, task, agent, sandbox: str, space: Optional[str] = None) -> Dict[str, str]:
         env = {k: os.environ[k] for k in ("PATH", "LANG", "LC_ALL", "TZ", "TMPDIR") if k in os.environ}
         env.update(self.extra_env)
         for v in task.info.command.environment.variables:
             if v.type == P.Environment.Variable.SECRET:
-                data = self._secret(v.secret)
+                data = self._secret(v.secret, space)
                 env[v.name] = data.decode("utf-8", "replace") if data is not None else ""
             else:
                 env[v.name] = v.value
