@@ -1,0 +1,90 @@
+"""LocalMaster behaviours the local DC/OS stand-in relies on, checked without a cluster:
+hierarchical-role offers, task addresses per network, mount disks added to a running agent."""
+import threading
+
+from dcos_commons_amd.mesos import protos as P
+from dcos_commons_amd.mesos.local_master import AgentSpec, LocalMaster, LocalSchedulerDriver
+
+
+class _Sink:
+    def __init__(self):
+        self.offers = []
+        self.got = threading.Event()
+
+    def resource_offers(self, driver, offers):
+        self.offers.extend(offers)
+        self.got.set()
+
+    def __getattr__(self, name):
+        return lambda *a, **kw: None
+
+
+def _framework(master, roles):
+    info = P.FrameworkInfo(name="fw", user="nobody")
+    if len(roles) > 1:
+        info.roles.extend(roles)
+        info.capabilities.add(type=P.FrameworkInfo.Capability.MULTI_ROLE)
+    else:
+        info.role = roles[0]
+    sink = _Sink()
+    driver = LocalSchedulerDriver(master, sink, info)
+    driver.start()
+    assert sink.got.wait(5)
+    return driver, sink
+
+
+def test_static_reservations_are_offered_to_sub_roles():
+    m = LocalMaster(allocation_interval_s=0.05)
+    try:
+        m.add_agent(AgentSpec(hostname="10.0.0.1", pre_reserved=(("slave_public", "cpus", 2.0),)))
+        _, sink = _framework(m, ["slave_public/svc-role", "svc-role"])
+        cpus = [r for r in sink.offers[0].resources if r.name == "cpus"]
+        static = [r for r in cpus if r.reservations]
+        unreserved = [r for r in cpus if not r.reservations]
+        # the slave_public reservation goes to the sub-role that can refine it
+        assert static and static[0].allocation_info.role == "slave_public/svc-role"
+        assert unreserved and unreserved[0].allocation_info.role in ("slave_public/svc-role", "svc-role")
+        # a framework of an unrelated role is never allocated it
+        other = type("Fw", (), {"roles": {"other-role"}})()
+        assert LocalMaster._alloc_role(other, "slave_public") is None
+        assert LocalMaster._alloc_role(other, "*") == "other-role"
+    finally:
+        m.shutdown()
+
+
+def test_task_addresses_follow_the_network():
+    m = LocalMaster(allocation_interval_s=0.05)
+    try:
+        aid = m.add_agent(AgentSpec(hostname="10.0.0.7"))
+        agent = m.agents[aid]
+        host = agent.task_networks(None)
+        assert [(n.name, n.ip_addresses[0].ip_address) for n in host] == [("", "10.0.0.7")]
+        c = P.ContainerInfo(type=P.ContainerInfo.MESOS)
+        ni = c.network_infos.add(name="dcos")
+        ni.labels.labels.add(key="k", value="v")
+        (overlay,) = agent.task_networks(c)
+        assert overlay.name == "dcos" and overlay.ip_addresses[0].ip_address.startswith("9.0.")
+        assert overlay.labels.labels[0].key == "k"
+        b = P.ContainerInfo(type=P.ContainerInfo.MESOS)
+        b.network_infos.add(name="mesos-bridge")
+        (bridge,) = agent.task_networks(b)
+        assert bridge.name == "mesos-bridge" and bridge.ip_addresses[0].ip_address == "10.0.0.7"
+        # non-IP hostnames fall back to the loopback address
+        other = m.agents[m.add_agent(AgentSpec(hostname="agent-b"))]
+        assert other.task_networks(None)[0].ip_addresses[0].ip_address == "127.0.0.1"
+    finally:
+        m.shutdown()
+
+
+def test_mount_disks_added_to_a_running_agent():
+    m = LocalMaster(allocation_interval_s=0.05)
+    try:
+        aid = m.add_agent(AgentSpec(hostname="10.0.0.1", mount_disks=(("/dcos/volume0", 100.0),)))
+        m.add_mount_disks(aid, [("/dcos/volume1", 200.0, "xfs")])
+        disks = {r.disk.source.mount.root: r for r in m.agent_resources(aid) if r.HasField("disk")
+                 and r.disk.source.type == P.Resource.DiskInfo.Source.MOUNT}
+        assert disks["/dcos/volume0"].scalar.value == 100.0 and not disks["/dcos/volume0"].disk.source.profile
+        assert disks["/dcos/volume1"].scalar.value == 200.0 and disks["/dcos/volume1"].disk.source.profile == "xfs"
+        assert len(m.agents[aid].spec.mount_disks) == 2
+    finally:
+        m.shutdown()
