@@ -25,7 +25,9 @@ APP_CONFIG_FIELD = "TASKCFG_ALL_HDFS_NAME_NODE_HANDLER_COUNT"
 @pytest.fixture(scope="module", autouse=True)
 def hdfs_cluster():
     c = make_cluster(executor="synthetic", finish_tasks=FINISH_TASKS)
-    sdk_install.install(PACKAGE, SVC, DEFAULT_TASK_COUNT)
+    # (data nodes pass their first readiness check after 1 s instead of the default 10 s)
+    sdk_install.install(PACKAGE, SVC, DEFAULT_TASK_COUNT,
+                        additional_options={"data_node": {"readiness_check": {"delay": 1, "interval": 1}}})
     yield c
     sdk_install.uninstall(PACKAGE, SVC)
     c.shutdown()
