@@ -62,13 +62,17 @@ class ProcessExit:
 # -- shutdown hooks (the JVM's Runtime.addShutdownHook: e.g. CuratorLocker releases the service lock
 #    so the next scheduler does not wait for the ZooKeeper session to expire) ---------------------
 _hooks = []
-_hooks_lock = threading.Lock()
+# re-entrant: the SIGTERM handler runs on the main thread, possibly while that same thread is inside
+# add_shutdown_hook/run_shutdown_hooks; a plain Lock would deadlock the process there
+_hooks_lock = threading.RLock()
 _hooks_ran = False
 
 
 def add_shutdown_hook(fn) -> None:
+    """Registers ``fn`` once (a hook added again is not run twice)."""
     with _hooks_lock:
-        _hooks.append(fn)
+        if fn not in _hooks:
+            _hooks.append(fn)
 
 
 def run_shutdown_hooks() -> None:

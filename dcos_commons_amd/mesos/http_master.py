@@ -303,10 +303,26 @@ class _Handler(BaseHTTPRequestHandler):
         self._reply(status, b"" if status == 202 else b"Call rejected: missing or stale Mesos-Stream-Id")
 
     def _peer_closed(self) -> bool:
+        """True only on evidence that the scheduler went away: EOF, reset or a poll error.
+
+        ``poll`` (not ``select``) so that descriptors >= FD_SETSIZE work in a master that holds
+        many sockets; the peek is non-blocking, and "nothing to read" means the peer is alive."""
         try:
-            r, _, _ = select.select([self.connection], [], [], 0)
-            return bool(r) and self.connection.recv(1, socket.MSG_PEEK) == b""
-        except (OSError, ValueError):
+            p = select.poll()
+            p.register(self.connection.fileno(), select.POLLIN | select.POLLPRI)
+            events = p.poll(0)
+        except (OSError, ValueError):  # fileno() of a closed socket
+            return True
+        if not events:
+            return False
+        mask = events[0][1]
+        if mask & (select.POLLERR | select.POLLNVAL):
+            return True
+        try:
+            return self.connection.recv(1, socket.MSG_PEEK | socket.MSG_DONTWAIT) == b""
+        except (BlockingIOError, InterruptedError):
+            return False
+        except OSError:
             return True
 
     def _stream(self, call: P.Call, accept: str) -> None:

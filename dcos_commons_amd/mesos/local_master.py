@@ -45,6 +45,7 @@ from dcos_commons_amd.mesos.resource_math import (
     pop_reservation,
     strip_volume,
 )
+from dcos_commons_amd.utils import ids
 
 LOGGER = logging.getLogger(__name__)
 TERMINAL = {P.TASK_FINISHED, P.TASK_FAILED, P.TASK_KILLED, P.TASK_ERROR, P.TASK_LOST, P.TASK_DROPPED,
@@ -627,7 +628,7 @@ class LocalMaster:
                     a.available.subtract(r)
                 for r in mine:
                     r.allocation_info.role = self._alloc_role(fw, effective_role(r))
-                oid = "offer-" + uuid.uuid4().hex
+                oid = "offer-" + ids.uuid4_hex()
                 self.offers[oid] = _Offer(oid, fw.id, a.id, mine)
                 o = P.Offer(hostname=a.spec.hostname)
                 o.id.value = oid
@@ -994,7 +995,7 @@ class LocalMaster:
             st.container_status.network_infos.extend(task.networks)
         else:
             st.container_status.network_infos.add().ip_addresses.add(ip_address="127.0.0.1")
-        st.uuid = uuid.uuid4().bytes
+        st.uuid = ids.uuid4_bytes()
         task.status = st
         if state in TERMINAL:
             task.epoch += 1

@@ -5,11 +5,11 @@ Reference: sdk/.../offer/CommonIdUtils.java. IDs are
 """
 from __future__ import annotations
 
-import uuid
 from typing import Optional
 
 from dcos_commons_amd.mesos import protos as P
 from dcos_commons_amd.offer.taskdata.labels import TaskException
+from dcos_commons_amd.utils import ids
 
 NAME_ID_DELIM = "__"
 
@@ -23,7 +23,7 @@ def _to_id_string(service_name: str, item_name: str) -> str:
         raise ValueError(f"Service cannot contain delimiter '{NAME_ID_DELIM}': {service_name}")
     if NAME_ID_DELIM in item_name:
         raise ValueError(f"Name cannot contain delimiter '{NAME_ID_DELIM}': {item_name}")
-    return f"{to_sanitized_service_name(service_name)}{NAME_ID_DELIM}{item_name}{NAME_ID_DELIM}{uuid.uuid4()}"
+    return f"{to_sanitized_service_name(service_name)}{NAME_ID_DELIM}{item_name}{NAME_ID_DELIM}{ids.uuid4_str()}"
 
 
 def to_task_id(service_name: str, task_name: str) -> P.TaskID:

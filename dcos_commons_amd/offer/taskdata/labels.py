@@ -14,6 +14,7 @@ import uuid
 from typing import Dict, List, Optional
 
 from dcos_commons_amd.mesos import protos as P
+from dcos_commons_amd.utils import ids
 
 BOOLEAN_LABEL_TRUE_VALUE = "true"
 TARGET_CONFIGURATION_LABEL = "target_configuration"
@@ -339,7 +340,7 @@ def set_dcos_space(executor_info: P.ExecutorInfo, space: str) -> None:
 
 def set_vip_labels(port: P.Port, vip_name: str, vip_port: int, network_names, supports_port_mapping) -> None:
     m = labels_to_map(port.labels)
-    m[f"{VIP_LABEL_PREFIX}{uuid.uuid4()}"] = f"{vip_name}:{vip_port}"
+    m[f"{VIP_LABEL_PREFIX}{ids.uuid4_str()}"] = f"{vip_name}:{vip_port}"
     if network_names:
         use_host_ip = any(supports_port_mapping(n) for n in network_names)
         m[VIP_OVERLAY_FLAG_KEY] = VIP_BRIDGE_FLAG_VALUE if use_host_ip else VIP_OVERLAY_FLAG_VALUE

@@ -13,6 +13,7 @@ from typing import Collection, Dict, Iterable, List, Optional, Set
 
 from dcos_commons_amd.offer import constants
 from dcos_commons_amd.scheduler.plan import backoff as backoff_mod
+from dcos_commons_amd.utils import ids
 
 from .pod_instance_requirement import PodInstanceRequirement
 from .status import Status
@@ -264,7 +265,7 @@ class Step(Element):
 
 class AbstractStep(Step):
     def __init__(self, name: str, namespace: Optional[str] = None):
-        self._id = uuid.uuid4()
+        self._id = ids.uuid4()
         self._name = name
         self._status = Status.PENDING
         self._interrupted = False
@@ -351,7 +352,7 @@ class AbstractStep(Step):
 
 class DefaultPhase(ParentElement):
     def __init__(self, name: str, steps: List[Step], strategy, errors: Optional[List[str]] = None):
-        self._id = uuid.uuid4()
+        self._id = ids.uuid4()
         self._name = name
         self._steps = list(steps)
         self._strategy = strategy
@@ -383,7 +384,7 @@ class DefaultPlan(ParentElement):
     def __init__(self, name: str, phases: List[DefaultPhase], strategy=None, errors: Optional[List[str]] = None):
         from .strategy import SerialStrategy
 
-        self._id = uuid.uuid4()
+        self._id = ids.uuid4()
         self._name = name
         self._phases = list(phases)
         self._strategy = strategy if strategy is not None else SerialStrategy()

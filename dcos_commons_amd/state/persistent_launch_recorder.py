@@ -5,10 +5,17 @@ is persisted *before* the ACCEPT is sent (empty-TaskID entries first), together 
 ``TASK_STAGING`` status for real launches; tasks sharing a resource set with the launched task get
 the new resources copied onto their stored TaskInfo.
 
-Addition: a launch whose TaskInfo references only reservations that no stored task of its pod
-instance referenced before this batch created its whole footprint (first launch or permanent
-replace). Its stored TaskInfo carries ``launch_new_footprint=true``; an in-place relaunch that
-reuses existing reservations or volumes never does.
+Addition: a launch whose task resources (its own resource set; the executor's resources are not
+considered) reference only reservations that no stored task of its pod instance referenced before
+this batch created its whole footprint (first launch or permanent replace). Its stored TaskInfo
+carries ``launch_new_footprint=true``; an in-place relaunch that reuses existing reservations or
+volumes never does.
+
+A pod's first footprint reserves every resource set of the pod, including those of tasks that
+only launch later (sidecars started by a plan, reference OfferEvaluator.java:411-536), and stores a
+TaskInfo (empty TaskID) for each of them. So the first launch of such a task reuses reservations
+that exist and is never labelled: a lost ACCEPT there is a transient LOST relaunched in place
+(``test_lost_accept_of_a_new_resource_set_next_to_a_running_executor_is_relaunched``).
 """
 from __future__ import annotations
 
@@ -49,7 +56,7 @@ class PersistentLaunchRecorder:
                 status.task_id.CopyFrom(info.task_id)
                 if info.HasField("executor"):
                     status.executor_id.CopyFrom(info.executor.executor_id)
-                ids = get_resource_ids(get_all_resources(info))
+                ids = get_resource_ids(info.resources)
                 new = bool(ids) and pi is not None and not (set(ids) & prior_ids.get(pi.name, set()))
                 TaskLabelWriter(info).set_launch_new_footprint(new).apply()
             if pi is not None:

@@ -256,7 +256,10 @@ def init_service_name(persister: Persister, service_name: str) -> None:
 class ZkLocker:
     """Exclusive per-service lease; one instance per process (``lock()``/``unlock()``)."""
     _instance: Optional["ZkLocker"] = None
-    _instance_lock = threading.Lock()
+    # re-entrant: ``unlock`` runs as a shutdown hook, possibly from a SIGTERM handler on a thread
+    # that is already inside ``lock``
+    _instance_lock = threading.RLock()
+    _hooks_registered = False
     enabled = True
 
     def __init__(self, service_name: str, connect: str, username: str = "", password: str = "",
@@ -272,23 +275,26 @@ class ZkLocker:
 
     @classmethod
     def lock(cls, service_name: str, connect: str, **kw) -> Optional["ZkLocker"]:
+        from dcos_commons_amd.framework.process_exit import ProcessExit, add_shutdown_hook
+
         with cls._instance_lock:
             if not cls.enabled:
                 return None
             if cls._instance is not None:
                 raise RuntimeError("Already locked")
             inst = cls(service_name, connect, **kw)
-            if not inst.lock_internal():
-                from dcos_commons_amd.framework.process_exit import ProcessExit
-
-                ProcessExit.exit(ProcessExit.LOCK_UNAVAILABLE)
-                return None
-            cls._instance = inst
-            atexit.register(cls.unlock)
-            from dcos_commons_amd.framework.process_exit import add_shutdown_hook
-
-            add_shutdown_hook(cls.unlock)
-            return inst
+            acquired = inst.lock_internal()
+            if acquired:
+                cls._instance = inst
+                if not cls._hooks_registered:  # once per process, however often lock() runs
+                    cls._hooks_registered = True
+                    atexit.register(cls.unlock)
+                    add_shutdown_hook(cls.unlock)
+        if not acquired:
+            # outside _instance_lock: the exit runs the shutdown hooks, and ``unlock`` needs that lock
+            ProcessExit.exit(ProcessExit.LOCK_UNAVAILABLE)
+            return None
+        return inst
 
     @classmethod
     def unlock(cls) -> None:

@@ -284,3 +284,60 @@ def test_never_launched_rule_applies_only_to_a_new_footprint():
         info = _stage_relaunch(c, "world-1-server", new_footprint=True)
         sched.process_status_update(_master_reply(info, P.TASK_DROPPED, P.TaskStatus.REASON_INVALID_OFFERS))
         assert TaskLabelReader(c.store.fetch_task("world-1-server")).is_permanently_failed()
+
+
+def test_lost_accept_of_a_new_resource_set_next_to_a_running_executor_is_relaunched():
+    """the first launch of a sidecar task (its own ``sidecar-res`` resource set) next to
+    a running server, with its ACCEPT lost. The pod's first footprint (the server's deploy) already
+    reserved ``sidecar-res`` (the new-footprint pipeline reserves every resource set of the pod, as
+    the reference's does), so this launch is not a new footprint: the watchdog's reconciliation
+    answers LOST, the task is relaunched in place on those reservations and the sidecar plan
+    completes; the server and its executor are never touched."""
+    from dcos_commons_amd.mesos.local_master import TaskBehavior, TaskTiming
+    from dcos_commons_amd.offer.resources import get_resource_ids
+    from dcos_commons_amd.offer.taskdata.labels import TaskLabelReader
+
+    env = dict(ENV, HELLO_COUNT="1")
+    cfg = SchedulerConfig.for_testing(PORT_API="0", SDK_OFFER_WAIT_S="0.2", SDK_LAUNCH_RECONCILE_S="0.3")
+    raw = RawServiceSpec.new_builder(os.path.join(SPECS, "sidecar.yml")).set_env(env).build()
+    spec = ServiceSpecGenerator(raw, cfg, SPECS, env).build()
+    once = TaskTiming(finish_after_s=0.05)
+    master = LocalMaster(allocation_interval_s=0.05,
+                         behavior=TaskBehavior(overrides={"backup": once, "verify": once}))
+    master.add_agent(AgentSpec(hostname="host-0", cpus=4, mem=8192, disk=20000))
+    runner = SchedulerRunner(SchedulerBuilder(spec, cfg, MemPersister()).set_plans_from(raw),
+                             driver_factory=lambda s, i: LocalSchedulerDriver(master, s, i))
+    runner.run(block=False)
+    try:
+        api = runner.framework_runner.api_server.router
+        store = runner.scheduler.state_store
+
+        def wait(pred, what, timeout=20.0):
+            t0 = time.time()
+            while time.time() - t0 < timeout:
+                if pred():
+                    return
+                time.sleep(0.005)
+            raise AssertionError(f"{what} not reached in {timeout}s")
+
+        wait(lambda: api.get("/v1/plans/deploy").status == 200, "deploy COMPLETE")
+        server = store.fetch_task("hello-0-server")
+        server_tid = server.task_id.value
+        reserved_at_deploy = sorted(get_resource_ids(store.fetch_task("hello-0-backup").resources))
+        assert reserved_at_deploy  # stored with an empty TaskID by the first footprint
+        master.drop_next_accepts(1)
+        assert api.post("/v1/plans/sidecar/start", body={}).status == 200
+        wait(lambda: master.dropped_accepts == 1, "backup ACCEPT dropped")
+        wait(lambda: api.get("/v1/plans/sidecar").status == 200, "sidecar plan COMPLETE")
+        backup = store.fetch_task("hello-0-backup")
+        assert not TaskLabelReader(backup).is_permanently_failed()
+        assert store.fetch_status("hello-0-backup").state == P.TASK_FINISHED
+        # the server and its executor were never touched
+        assert store.fetch_task("hello-0-server").task_id.value == server_tid
+        assert master.task_states()[server_tid] == P.TASK_RUNNING
+        assert backup.executor.executor_id.value == server.executor.executor_id.value
+        assert not TaskLabelReader(backup).is_launch_new_footprint()
+        assert sorted(get_resource_ids(backup.resources)) == reserved_at_deploy
+    finally:
+        runner.stop()
+        master.shutdown()

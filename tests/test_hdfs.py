@@ -247,3 +247,22 @@ def test_replace_journal_and_data():
         Expect.that(check, "journal replaced via override, data via default recovery"),
     ]
     runner().run(ticks)
+
+
+@pytest.mark.parametrize("framework,pods", [("hdfs", ("journal", "name", "data")), ("cassandra", ("node",))])
+@pytest.mark.parametrize("labels,expected", [("", ()), ("k_0:v_0,k_1:v_1", (("k_0", "v_0"), ("k_1", "v_1")))])
+def test_virtual_network_plugin_labels_reach_every_pod(framework, pods, labels, expected):
+    """the reference passes ``virtual_network_plugin_labels`` (config.json:45) as CNI
+    labels on every overlay-network pod (hdfs svc.yml:23-27,170-174,476-480; cassandra svc.yml:9-13)."""
+    r = ServiceTestRunner.for_framework(framework)
+    for pod in pods:
+        if framework == "hdfs":
+            r.set_pod_env(pod, SERVICE_ZK_ROOT="/dcos-service-hdfs", DECODED_AUTH_TO_LOCAL="")
+        else:
+            r.set_pod_env(pod, {"LOCAL_SEEDS": "a,b"})
+    r = r.set_options("service.virtual_network_enabled", "true", "service.virtual_network_name", "dcos",
+                      "service.virtual_network_plugin_labels", labels).run()
+    for pod in pods:
+        nets = r.service_spec.pod(pod).networks
+        assert [n.name for n in nets] == ["dcos"]
+        assert tuple(sorted(nets[0].labels)) == expected

@@ -212,6 +212,81 @@ def test_stream_loss_disconnects_or_fails_over(cluster):
         d2.stop()
 
 
+def _raw_subscribe(hm, name="raw"):
+    """SUBSCRIBE over a bare socket; returns (socket, framework_id) once SUBSCRIBED arrived."""
+    import socket as _socket
+
+    call = P.Call(type=P.Call.SUBSCRIBE)
+    call.subscribe.framework_info.name = name
+    call.subscribe.framework_info.role = "r"
+    body = encode_message(call, JSON)
+    s = _socket.create_connection(("127.0.0.1", hm.port), timeout=5)
+    s.sendall(b"POST /api/v1/scheduler HTTP/1.1\r\nHost: x\r\nContent-Type: application/json\r\n"
+              b"Accept: application/json\r\nContent-Length: %d\r\n\r\n%s" % (len(body), body))
+    buf = b""
+    deadline = time.time() + 5
+    while b"SUBSCRIBED" not in buf and time.time() < deadline:
+        buf += s.recv(65536)
+    assert b"SUBSCRIBED" in buf, buf
+    deadline = time.time() + 5
+    while not hm.subscriptions and time.time() < deadline:
+        time.sleep(0.01)
+    return s, next(iter(hm.subscriptions))
+
+
+def _connected(lm, fid):
+    fw = lm.call(lambda: lm.frameworks.get(fid))
+    return fw is not None and fw.connected
+
+
+def test_closed_client_socket_disconnects_the_framework_within_a_second(cluster):
+    """the master notices a scheduler whose connection closed (EOF on the stream
+    socket) at its next idle poll, not at the next heartbeat write."""
+    lm, hm = cluster
+    hm.heartbeat_s = 30.0  # no heartbeat write can be what detects the close
+    s, fid = _raw_subscribe(hm)
+    assert _connected(lm, fid)
+    t0 = time.time()
+    s.close()
+    while _connected(lm, fid) and time.time() - t0 < 3:
+        time.sleep(0.02)
+    assert not _connected(lm, fid)
+    assert time.time() - t0 < 1.0 + 0.5  # one 0.25 s idle poll + scheduling slack
+    assert fid not in hm.subscriptions
+
+
+def test_stream_survives_when_master_holds_more_than_fd_setsize_descriptors(cluster):
+    """with >= 1024 open descriptors ``select`` raised ValueError, which read as
+    'peer closed' and dropped every stream after its first idle poll."""
+    import os
+    import resource
+
+    lm, hm = cluster
+    hm.heartbeat_s = 30.0
+    soft, hard = resource.getrlimit(resource.RLIMIT_NOFILE)
+    if hard != resource.RLIM_INFINITY and hard < 1200:
+        pytest.skip(f"RLIMIT_NOFILE hard limit {hard} < 1200")
+    if soft != resource.RLIM_INFINITY and soft < 1200:
+        resource.setrlimit(resource.RLIMIT_NOFILE, (1200, hard))
+    held = []
+    try:
+        while not held or held[-1] < 1030:
+            held.append(os.open(os.devnull, os.O_RDONLY))
+        s, fid = _raw_subscribe(hm)
+        stream_sock_fd = hm.subscriptions[fid]  # noqa: F841 (the server-side socket is > 1024 now)
+        time.sleep(1.2)  # several idle polls
+        assert _connected(lm, fid)
+        s.close()
+        t0 = time.time()
+        while _connected(lm, fid) and time.time() - t0 < 3:
+            time.sleep(0.02)
+        assert not _connected(lm, fid)
+    finally:
+        for fd in held:
+            os.close(fd)
+        resource.setrlimit(resource.RLIMIT_NOFILE, (soft, hard))
+
+
 def test_failover_recovers_offers_held_by_the_previous_instance(cluster):
     """A scheduler that re-subscribes with its FrameworkID while the master still counts offers as
     outstanding to the old instance gets those resources offered again (Mesos rescinds them on

@@ -235,3 +235,65 @@ def test_factory_zk_and_file_backends_take_the_lock(zk, tmp_path):
     FileLocker._held[other.path].unlock()
     assert other.lock()
     other.unlock()
+
+
+def test_lock_failure_exits_outside_the_instance_lock_and_hooks_register_once(zk, monkeypatch):
+    """ADVICE r2: ``ZkLocker.lock`` called ``ProcessExit.exit`` while holding ``_instance_lock``;
+    the exit runs ``unlock`` as a shutdown hook, which needs that lock. The hook was also appended
+    on every ``lock()``."""
+    from dcos_commons_amd.framework import process_exit as PE
+
+    monkeypatch.setattr(PE, "_hooks", [])
+    monkeypatch.setattr(ZkLocker, "_hooks_registered", False)
+    free_at_exit = []
+
+    def fake_exit(code, cause=None):
+        got = []
+
+        def probe():
+            ok = ZkLocker._instance_lock.acquire(timeout=1)
+            if ok:
+                ZkLocker._instance_lock.release()
+            got.append(ok)
+
+        th = threading.Thread(target=probe)
+        th.start()
+        th.join(2)
+        free_at_exit.append(bool(got and got[0]))
+        raise ProcessExitError(code, cause)
+
+    monkeypatch.setattr(ProcessExit, "exit", staticmethod(fake_exit))
+    holder = ZkLocker("svc4", zk.connect_string)
+    assert holder.lock_internal()
+    with pytest.raises(ProcessExitError):
+        ZkLocker.lock("svc4", zk.connect_string, wait_s=0.05)
+    assert free_at_exit == [True]
+    holder.unlock_internal()
+    for _ in range(3):
+        ZkLocker.lock("svc4", zk.connect_string, wait_s=1)
+        ZkLocker.unlock()
+    assert PE._hooks.count(ZkLocker.unlock) == 1
+
+
+def test_shutdown_hooks_run_from_a_handler_that_interrupts_hook_registration(monkeypatch):
+    """SIGTERM landing while the main thread is inside ``add_shutdown_hook`` ran the
+    hooks under a non-reentrant lock already held by that thread (deadlock)."""
+    from dcos_commons_amd.framework import process_exit as PE
+
+    monkeypatch.setattr(PE, "_hooks", [])
+    monkeypatch.setattr(PE, "_hooks_ran", False)
+    ran = []
+    PE.add_shutdown_hook(lambda: ran.append(1))
+    done = threading.Event()
+
+    def body():
+        with PE._hooks_lock:  # the interrupted add_shutdown_hook
+            PE.run_shutdown_hooks()  # what the signal handler runs on the same thread
+        done.set()
+
+    th = threading.Thread(target=body, daemon=True)
+    th.start()
+    assert done.wait(2), "run_shutdown_hooks deadlocked on the hooks lock"
+    assert ran == [1]
+    PE.run_shutdown_hooks()  # at most once
+    assert ran == [1]
