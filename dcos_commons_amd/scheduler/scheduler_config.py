@@ -22,8 +22,16 @@ def _scalar(v: float) -> P.Value:
 
 
 class SchedulerConfig:
+    _printed_build_info = False
+
     def __init__(self, env_store: Optional[EnvStore] = None):
         self.env = env_store or EnvStore.from_env()
+        if not SchedulerConfig._printed_build_info:  # once per process (SchedulerConfig.java:322-324)
+            SchedulerConfig._printed_build_info = True
+            import json
+            import logging
+
+            logging.getLogger(__name__).info("Build information:\n%s", json.dumps(self.build_info(), indent=2))
 
     @staticmethod
     def from_env() -> "SchedulerConfig":
@@ -290,10 +298,21 @@ class SchedulerConfig:
     def implicit_reconcile_period_s(self) -> float:
         return self.implicit_reconcile_period_ms() / 1000.0
 
+    def package_build_time_ms(self) -> int:
+        return self.env.get_optional_int("PACKAGE_BUILD_TIME_EPOCH_MS", 0)
+
     def build_info(self) -> Dict[str, str]:
+        """Reference SchedulerConfig.getBuildInfo (SchedulerConfig.java:655-665): package identity
+        plus the SDK's own build stamp (``sdk_build_info``), served by the multi-service
+        ``/v1/health`` and logged once per process."""
+        from dcos_commons_amd.utils import sdk_build_info as B
+
         return {
             "PACKAGE_NAME": self.env.get_optional("PACKAGE_NAME", ""),
             "PACKAGE_VERSION": self.env.get_optional("PACKAGE_VERSION", ""),
-            "SDK_NAME": "dcos-commons-amd",
-            "SDK_VERSION": "0.58.0-mi355x",
+            "PACKAGE_BUILT_AT": B.iso_instant(self.package_build_time_ms()),
+            "SDK_NAME": B.NAME,
+            "SDK_VERSION": B.VERSION,
+            "SDK_GIT_SHA": B.git_sha(),
+            "SDK_BUILT_AT": B.iso_instant(B.build_time_ms()),
         }
