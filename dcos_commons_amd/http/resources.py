@@ -268,11 +268,32 @@ class GroupedTasks:
         return None
 
 
+def set_pods_permanently_failed(config_store, state_store, task_infos) -> None:
+    """Default ``replace`` failure setter (reference PodQueries.FailureSetter, PodQueries.java:438):
+    stamps ``permanently-failed`` on every task of each pod instance the launched tasks belong to.
+    Stub tasks that were never launched (empty TaskID) are skipped."""
+    from dcos_commons_amd.scheduler.recovery import set_pod_permanently_failed
+
+    pods = {}
+    for info in task_infos:
+        if not info.task_id.value:
+            LOGGER.info("Not marking task %s as failed due to empty taskId", info.name)
+            continue
+        try:
+            pi = get_pod_instance(config_store, info)
+            pods[pi.name] = pi
+        except (TaskException, ValueError, ConfigStoreException):
+            LOGGER.exception("Failed to get pod for task %s", info.task_id.value)
+    for pi in pods.values():
+        set_pod_permanently_failed(state_store, pi)
+
+
 class PodResource:
-    def __init__(self, state_store, config_store, service_name: str):
+    def __init__(self, state_store, config_store, service_name: str, failure_setter=None):
         self.state_store = state_store
         self.config_store = config_store
         self.service_name = service_name
+        self.failure_setter = failure_setter or set_pods_permanently_failed
 
     def routes(self) -> List[Route]:
         return [
@@ -378,20 +399,10 @@ class PodResource:
                     backoff.get_instance().clear_delay(to_task_name(info.task_id))
                 except (TaskException, ValueError):
                     pass
+        LOGGER.info("Performing %s of pod %s by killing %d tasks", "replace" if recovery_type == RecoveryType.PERMANENT
+                    else "restart", name, len(tasks))
         if recovery_type == RecoveryType.PERMANENT:
-            from dcos_commons_amd.scheduler.recovery import set_pod_permanently_failed
-
-            pods = {}
-            for info, _ in tasks:
-                if not info.task_id.value:
-                    continue
-                try:
-                    pi = get_pod_instance(self.config_store, info)
-                    pods[pi.name] = pi
-                except (TaskException, ValueError, ConfigStoreException):
-                    LOGGER.exception("Failed to get pod for task %s", info.task_id.value)
-            for pi in pods.values():
-                set_pod_permanently_failed(self.state_store, pi)
+            self.failure_setter(self.config_store, self.state_store, [info for info, _ in tasks])
         return self._kill(name, tasks)
 
     @staticmethod
