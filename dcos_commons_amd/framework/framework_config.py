@@ -9,6 +9,9 @@ from typing import List, Optional
 
 from dcos_commons_amd.storage.persister_utils import with_escaped_slashes
 
+SLASH_REPLACEMENT = "__"
+_FROM_ENV = object()
+
 DEFAULT_ROLE_SUFFIX = "-role"
 DEFAULT_PRINCIPAL_SUFFIX = "-principal"
 DEFAULT_SERVICE_USER = "root"
@@ -66,8 +69,15 @@ class FrameworkConfig:
             web_url=spec.web_url)
 
     @staticmethod
-    def from_env_store(env, namespace: Optional[str] = None) -> "FrameworkConfig":
+    def from_env_store(env, namespace: Optional[str] = _FROM_ENV) -> "FrameworkConfig":
+        """Multi-service mode: identity from the scheduler's environment. The service namespace
+        (role) comes from ``MESOS_ALLOCATION_ROLE`` / ``MARATHON_APP_ENFORCE_GROUP_ROLE`` as
+        SchedulerConfig.getServiceNamespace decides it, unless one is passed explicitly."""
         name = env.get_required("FRAMEWORK_NAME")
+        if namespace is _FROM_ENV:
+            from dcos_commons_amd.scheduler.scheduler_config import SchedulerConfig
+
+            namespace = SchedulerConfig(env).service_namespace()
         return FrameworkConfig(
             framework_name=name,
             role=_service_role(name, namespace),
@@ -83,3 +93,9 @@ class FrameworkConfig:
 
     def non_namespaced_role(self) -> str:
         return with_escaped_slashes(self.framework_name) + DEFAULT_ROLE_SUFFIX
+
+    def namespaced_role(self) -> Optional[str]:
+        """The top-level Marathon group of the service (``/path/to/svc`` -> ``path``), the quota role
+        a group-role migration moves to; None outside a group (FrameworkConfig.getNamespacedRole)."""
+        groups = self.non_namespaced_role().split(SLASH_REPLACEMENT)
+        return groups[0] if len(groups) > 1 else None

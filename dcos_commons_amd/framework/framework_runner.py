@@ -6,8 +6,10 @@ any pod asks for GPUs, RESERVATION_REFINEMENT, REGION_AWARE), starts the API ser
 declined until it is up), creates the driver and blocks on it. With uninstall enabled and no
 stored FrameworkID it wipes the state and serves an empty deploy plan ("skeleton scheduler").
 
-Drivers: ``driver_factory(scheduler, framework_info) -> driver``. The default picks from
-``SDK_MESOS_MASTER``: ``local`` (in-process ``LocalMaster``) or an ``http://host:port`` v1 master.
+Drivers: ``driver_factory(scheduler, framework_info) -> driver``. The default
+(``scheduler_driver_factory``) picks from ``SDK_MESOS_MASTER``: ``local`` (in-process
+``LocalMaster``) or an ``http://host:port`` / ``zk://`` v1 master, with the reference's credential
+rules.
 """
 from __future__ import annotations
 
@@ -46,8 +48,11 @@ class FrameworkRunner:
     def resource_roles(self) -> Set[str]:
         roles = {self.framework_config.role}
         roles.update(self.framework_config.pre_reserved_roles)
-        if self.scheduler_config.enable_role_migration():
+        if self.scheduler_config.enable_role_migration():  # both the legacy and the group (quota) role
             roles.add(self.framework_config.non_namespaced_role())
+            ns = self.framework_config.namespaced_role()
+            if ns is not None:
+                roles.add(ns)
         return roles
 
     def get_framework_info(self, framework_id: Optional[P.FrameworkID]) -> P.FrameworkInfo:
@@ -76,20 +81,9 @@ class FrameworkRunner:
         return info
 
     def _default_driver_factory(self):
-        master = self.scheduler_config.mesos_master_url()
-        if master.startswith(("http://", "https://", "zk://")):
-            from dcos_commons_amd.mesos.http_driver import V1HttpSchedulerDriver, resolve_master_url
+        from .scheduler_driver_factory import default_driver_factory
 
-            master = resolve_master_url(master)
-
-            cfg = self.scheduler_config
-            return lambda sched, info: V1HttpSchedulerDriver(
-                master, sched, info, credential=cfg.mesos_credential(), content_type=cfg.mesos_content_type(),
-                reconnect=cfg.is_driver_reconnect())
-        from dcos_commons_amd.mesos.local_master import LocalSchedulerDriver, local_master_from_env
-
-        lm = local_master_from_env(self.scheduler_config.env)
-        return lambda sched, info: LocalSchedulerDriver(lm, sched, info)
+        return default_driver_factory(self.scheduler_config)
 
     def start(self, persister, client, block: bool = True):
         """Registers and (if ``block``) runs until the driver stops. Returns the driver otherwise."""

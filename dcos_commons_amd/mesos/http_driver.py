@@ -71,7 +71,7 @@ class V1HttpSchedulerDriver(SchedulerDriver):
                  credential: Optional[P.Credential] = None, content_type: str = PROTOBUF,
                  implicit_acknowledgements: bool = True, reconnect: bool = False,
                  heartbeat_misses: int = 5, connect_timeout_s: float = 10.0,
-                 backoff_s: float = 0.5, max_backoff_s: float = 10.0):
+                 backoff_s: float = 0.5, max_backoff_s: float = 10.0, token_provider=None):
         if content_type not in (PROTOBUF, JSON):
             raise ValueError(f"unsupported content type {content_type}")
         self.master_url = master_url.rstrip("/")
@@ -79,6 +79,8 @@ class V1HttpSchedulerDriver(SchedulerDriver):
         self.framework_info = P.FrameworkInfo()
         self.framework_info.CopyFrom(framework_info)
         self.credential = credential
+        # side-channel auth: a principal-only credential plus a DC/OS IAM token per call
+        self.token_provider = token_provider
         self.content_type = content_type
         self.implicit_acknowledgements = implicit_acknowledgements
         self.reconnect = reconnect
@@ -203,7 +205,10 @@ class V1HttpSchedulerDriver(SchedulerDriver):
     # -- transport ---------------------------------------------------------------------
     def _headers(self, accept: str) -> dict:
         h = {"Content-Type": self.content_type, "Accept": accept, "Connection": "keep-alive"}
-        if self.credential is not None and self.credential.principal:
+        if self.token_provider is not None:
+            tok = self.token_provider()
+            h["Authorization"] = "token=" + (tok.value if hasattr(tok, "value") else str(tok))
+        elif self.credential is not None and self.credential.principal:
             token = f"{self.credential.principal}:{self.credential.secret or ''}".encode("utf-8")
             h["Authorization"] = "Basic " + base64.b64encode(token).decode("ascii")
         return h

@@ -183,6 +183,8 @@ class SchedulerConfig:
         return self.env.get_optional_boolean("SDK_DRIVER_RECONNECT", False)
 
     def mesos_credential(self):
+        """Principal + secret from ``SDK_MESOS_PRINCIPAL``/``SDK_MESOS_SECRET`` (tools and tests that
+        build a driver by hand; the scheduler itself uses SchedulerDriverFactory's rules)."""
         principal = self.env.get_optional("SDK_MESOS_PRINCIPAL", "")
         if not principal:
             return None
