@@ -424,7 +424,12 @@ class OfferProcessor:
         self.merge_agent_offers = merge_agent_offers
         # ACCEPT each step's launch as soon as it is matched instead of after the whole cycle
         self.stream_launches = stream_launches
-        self._held: Dict[str, tuple] = {}  # (real) offer id -> (offer, hold deadline)
+        # (real) offer id -> (offer, hold deadline). Rescinds arrive on the driver's thread while
+        # the offer thread evaluates, so the map is only touched under _held_lock, and an offer
+        # rescinded mid-cycle is remembered so that the cycle does not hold it again.
+        self._held: Dict[str, tuple] = {}
+        self._held_lock = threading.Lock()
+        self._rescinded: set = set()
         self._initialized = False
         self._deregistered = False
         self._in_progress = set()
@@ -488,8 +493,15 @@ class OfferProcessor:
             self.process_queued_offers(0)
 
     def dequeue(self, offer_id: P.OfferID) -> None:
+        """The master rescinded ``offer_id``: drop it from the queue and from the held set."""
         self.queue.remove(offer_id)
-        self._held.pop(offer_id.value, None)
+        with self._held_lock:
+            self._held.pop(offer_id.value, None)
+            self._rescinded.add(offer_id.value)
+
+    def held_offer_ids(self) -> List[str]:
+        with self._held_lock:
+            return list(self._held)
 
     def await_offers_processed(self, timeout_s: float = 5.0) -> None:
         deadline = time.monotonic() + timeout_s
@@ -501,11 +513,16 @@ class OfferProcessor:
         raise TimeoutError("Timed out waiting for offers to be processed")
 
     def process_queued_offers(self, wait_s: float) -> None:
+        with self._held_lock:
+            # rescinds from earlier cycles concern offers that are gone by now; from here on, a
+            # rescind of an offer this cycle takes is recorded and honoured when the cycle ends
+            self._rescinded.clear()
         new_offers = self.queue.take_all(wait_s, self._wake if self.event_driven else None)
         if self._stop.is_set():
             return
         now = time.monotonic()
-        held = [o for o, _ in self._held.values()]
+        with self._held_lock:
+            held = [o for o, _ in self._held.values()]
         offers = held + new_offers
         self.cycles += 1
         try:
@@ -527,10 +544,12 @@ class OfferProcessor:
                         self._wake.set()
                 elif self._deregistered:
                     # the framework was just torn down: its offers went with it
-                    self._held.clear()
+                    with self._held_lock:
+                        self._held.clear()
                     return
                 elif offers:
-                    self._held.clear()
+                    with self._held_lock:
+                        self._held.clear()
                     if self.gc_all_offers:
                         offers = self._collect_garbage(offers)
                     decline_long(offers)
@@ -617,28 +636,32 @@ class OfferProcessor:
             cleanup_recs = to_cleanup_recommendations(un.offer_resources)
             unused = filter_out_accepted(unused, cleanup_recs)
         used = {o.id.value for o in real(offers)} - {o.id.value for o in real(unused)}
-        for oid in used:
-            self._held.pop(oid, None)
         unused = real(unused)
-        if unused:
-            if resp.result == OfferResult.PROCESSED and cleanup_result == UnexpectedResult.PROCESSED:
-                if self.hold_s > 0:
-                    to_decline = []
-                    for o in unused:
-                        prev = self._held.get(o.id.value)
-                        deadline = prev[1] if prev is not None else now + self.hold_s
-                        if deadline <= now:
-                            self._held.pop(o.id.value, None)
-                            to_decline.append(o)
-                        else:
-                            self._held[o.id.value] = (o, deadline)
-                    decline_short(to_decline)
+        to_decline_short, to_decline_long = [], []
+        with self._held_lock:
+            for oid in used:
+                self._held.pop(oid, None)
+            # a rescinded offer is gone from the master: neither held nor declined
+            unused = [o for o in unused if o.id.value not in self._rescinded]
+            if unused:
+                if resp.result == OfferResult.PROCESSED and cleanup_result == UnexpectedResult.PROCESSED:
+                    if self.hold_s > 0:
+                        for o in unused:
+                            prev = self._held.get(o.id.value)
+                            deadline = prev[1] if prev is not None else now + self.hold_s
+                            if deadline <= now:
+                                self._held.pop(o.id.value, None)
+                                to_decline_short.append(o)
+                            else:
+                                self._held[o.id.value] = (o, deadline)
+                    else:
+                        to_decline_long = unused
                 else:
-                    decline_long(unused)
-            else:
-                for o in unused:
-                    self._held.pop(o.id.value, None)
-                decline_short(unused)
+                    for o in unused:
+                        self._held.pop(o.id.value, None)
+                    to_decline_short = unused
+        decline_short(to_decline_short)
+        decline_long(to_decline_long)
         if resp.streamed:
             all_recs = [r for r in pre_cleanup if id(r) not in streamed_pre] + cleanup_recs
         else:
@@ -648,8 +671,9 @@ class OfferProcessor:
 
     def release_held(self) -> None:
         """Decline every held offer (e.g. when the scheduler goes idle or stops)."""
-        held = [o for o, _ in self._held.values()]
-        self._held.clear()
+        with self._held_lock:
+            held = [o for o, _ in self._held.values()]
+            self._held.clear()
         decline_short(held)
 
     def _destroy_framework(self) -> None:

@@ -432,3 +432,53 @@ def test_unknown_task_status_kills_once(drv):
     ok.task_id.value = "known"
     fs.status_update(drv, ok)
     assert drv.kills == ["stray"] and c.statuses == ["stray", "stray", "known"]
+
+
+def test_offer_rescinded_during_its_cycle_is_neither_held_nor_declined(drv):
+    """A rescind (driver thread) that lands while the offer thread evaluates the offer: the cycle
+    must not hold the dead offer again (it would be re-evaluated and ACCEPTed after the master
+    dropped it) nor decline it."""
+    c = Client()
+    p = processor(c, hold_s=10.0).disable_threading()
+    p.start()
+
+    def rescinding(offers):
+        for o in offers:
+            if o.id.value == "a":
+                p.dequeue(o.id)
+        return OfferResponse.processed([])
+    c.offers_fn = rescinding
+    p.enqueue([offer("a"), offer("b")])
+    assert p.held_offer_ids() == ["b"]
+    assert drv.declines == []
+
+
+def test_held_offers_survive_concurrent_rescinds(drv):
+    """Rescinds hammering the processor from another thread while cycles run over held offers
+    (the held map used to be iterated unguarded: 'dictionary changed size during iteration')."""
+    import threading as _t
+
+    c = Client()
+    p = processor(c, hold_s=60.0).disable_threading()
+    p.start()
+    stop = _t.Event()
+    errors = []
+
+    def rescinder():
+        i = 0
+        while not stop.is_set():
+            p.dequeue(P.OfferID(value=f"o{i % 200}"))
+            i += 1
+
+    t = _t.Thread(target=rescinder, daemon=True)
+    t.start()
+    try:
+        for n in range(60):
+            try:
+                p.enqueue([offer(f"o{(n * 7 + k) % 200}") for k in range(20)])
+            except RuntimeError as e:  # pragma: no cover - the regression
+                errors.append(e)
+    finally:
+        stop.set()
+        t.join()
+    assert errors == []
