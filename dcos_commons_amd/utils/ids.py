@@ -20,6 +20,17 @@ _buf = b""
 _pos = 0
 
 
+def _reset_after_fork() -> None:
+    """A forked child must not replay its parent's pooled random bytes (duplicate IDs)."""
+    global _buf, _pos, _lock
+    _lock = threading.Lock()
+    _buf, _pos = b"", 0
+
+
+if hasattr(os, "register_at_fork"):
+    os.register_at_fork(after_in_child=_reset_after_fork)
+
+
 def _random16() -> bytearray:
     global _buf, _pos
     with _lock:
