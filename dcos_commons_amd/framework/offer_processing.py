@@ -95,6 +95,11 @@ class OfferQueue:
         with self._cond:
             return len(self._q)
 
+    def remaining_capacity(self) -> int:
+        """Free slots (OfferQueue.getRemainingCapacity); unbounded queues report -1."""
+        with self._cond:
+            return self.capacity - len(self._q) if self.capacity else -1
+
 
 class TokenBucket:
     """Revive rate limiter: capacity 256, +1 token every 256 s, >= 5 s between acquires
@@ -158,6 +163,11 @@ class TokenBucket:
             if self.count <= 0:
                 wait = max(wait, self.increment_interval_s - (now - self._last_increment))
             return wait
+
+    def increment(self) -> None:
+        """Adds one token now, up to the capacity (the reference's refill-thread tick)."""
+        with self._lock:
+            self.count = min(self.capacity, self.count + 1)
 
     def reset(self) -> None:
         with self._lock:
