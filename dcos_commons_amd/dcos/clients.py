@@ -43,7 +43,8 @@ def master_uri() -> str:
 
 class DcosHttpError(IOError):
     def __init__(self, status: int, reason: str, body: str = ""):
-        super().__init__(f"HTTP {status} {reason}: {body[:200]}")
+        # "<code> - <reason>" and "code=<code>" as the reference's clients word it
+        super().__init__(f"{status} - {reason} (code={status})" + (f": {body[:200]}" if body else ""))
         self.status = status
         self.reason = reason
         self.body = body
@@ -247,7 +248,13 @@ class DcosVersionClient:
         self.url = (base_uri or master_uri()) + "/dcos-metadata/dcos-version.json"
 
     def get_version(self) -> str:
+        return self.get_dcos_version().version
+
+    def get_dcos_version(self):
+        """The version document as a ``DcosVersion`` (version string + variant)."""
+        from dcos_commons_amd.dcos.capabilities import DcosVersion
+
         status, body = self.executor.execute("GET", self.url)
         if status != 200:
             raise DcosHttpError(status, "version lookup failed")
-        return json.loads(body)["version"]
+        return DcosVersion.from_json(body)

@@ -199,7 +199,8 @@ class VolumeSpec(ResourceSpec):
                  f"Volume container-path '{self.container_path}' must match "
                  f"{self._VALID_PATH.pattern}")
         for p in self.profiles:
-            _require(bool(self._VALID_PROFILE.fullmatch(p)), f"Invalid volume profile '{p}'")
+            _require(isinstance(p, str) and bool(self._VALID_PROFILE.fullmatch(p)), f"Invalid volume profile '{p}'")
+        _require(len(set(self.profiles)) == len(self.profiles), f"Duplicate volume profiles: {list(self.profiles)}")
         if self.type == VolumeType.ROOT:
             _require(not self.profiles, f"ROOT volume '{self.container_path}' cannot have profiles")
 
@@ -504,9 +505,11 @@ class HealthCheckSpec:
             _require(v is not None and v >= 0, f"health check {n} must be >= 0")
 
     def to_dict(self):
+        # "gracePeriod" is written too so that an older scheduler can still read the config
+        # (DefaultHealthCheckSpec.getGracePeriodForDowngradeCompatibility)
         return {"command": self.command, "max-consecutive-failures": self.max_consecutive_failures,
                 "delay": self.delay, "interval": self.interval, "timeout": self.timeout,
-                "grace-period": self.grace_period}
+                "grace-period": self.grace_period, "gracePeriod": self.grace_period}
 
     @staticmethod
     def from_dict(d):
@@ -884,6 +887,12 @@ class PodSpec:
 class ReplacementFailurePolicy:
     permanent_failure_timeout_mins: int = 20
     min_replace_delay_mins: int = 10
+
+    def validate(self) -> None:
+        _require(self.permanent_failure_timeout_mins is not None and self.permanent_failure_timeout_mins >= 0,
+                 "permanent-failure-timeout-mins must be >= 0")
+        _require(self.min_replace_delay_mins is not None and self.min_replace_delay_mins >= 0,
+                 "min-replace-delay-mins must be >= 0")
 
     def to_dict(self):
         return {"permanent-failure-timeout-mins": self.permanent_failure_timeout_mins,

@@ -119,7 +119,7 @@ def _verify_distinct_endpoint_names(raw_pods) -> None:
         for rs in (pod.get("resource-sets") or {}).values():
             collect(rs.get("ports"))
     if dups:
-        raise SpecValidationError(f"Service has duplicate advertised ports across tasks: {sorted(dups)}")
+        raise SpecValidationError(f"Service has duplicate advertised ports across tasks: [{', '.join(sorted(dups))}]")
 
 
 def _pod_role(pre_reserved_role: Optional[str], role: str) -> str:
@@ -268,7 +268,7 @@ def _convert_task(rt, reader: ConfigTemplateReader, task_name, additional_env, r
     goal_str = (rt.get("goal") or "").upper()
     if goal_str == "FINISHED":
         raise SpecValidationError(
-            f"Unsupported GoalState {goal_str} in task {task_name}, expected one of: {[g.value for g in GoalState]}")
+            f"Unsupported GoalState {goal_str} in task {task_name}, expected one of: [{', '.join(g.value for g in GoalState)}]")
     try:
         goal = GoalState(goal_str)
     except ValueError:

@@ -31,7 +31,7 @@ def _construct_mapping(loader, node, deep=False):
         if not isinstance(key, str):
             key = str(key)
         if key in out:
-            raise RawSpecError(f"Duplicate key: {key} (line {key_node.start_mark.line + 1})")
+            raise RawSpecError(f"Duplicate field '{key}' (line {key_node.start_mark.line + 1})")
         out[key] = loader.construct_object(value_node, deep=deep)
     return out
 

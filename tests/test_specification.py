@@ -105,7 +105,7 @@ def test_gpu_resource_fixture():
 def test_duplicate_keys_are_an_error():
     with pytest.raises(Exception) as e:
         build(os.path.join(FIXTURES, "invalid-duplicate-count.yml"))
-    assert "Duplicate key: count" in str(e.value)
+    assert "Duplicate field 'count'" in str(e.value)
 
 
 # -- mustache ---------------------------------------------------------------------------------
