@@ -226,6 +226,9 @@ class RangeSpec:
     begin: int
     end: int
 
+    MIN_PORT = 0
+    MAX_PORT = 65535
+
     def to_dict(self):
         return {"begin": self.begin, "end": self.end}
 

@@ -142,8 +142,9 @@ def _convert_ports(role, pre_reserved_role, principal, raw_ports, network_names)
                       env_key=rp.get("env-key"), port_name=name, visibility=visibility,
                       network_names=tuple(network_names))
         # RangeSpec: a missing begin is MIN_PORT (0); a missing or zero end is MAX_PORT (65535)
-        ranges = tuple(RangeSpec(int(r["begin"]) if r.get("begin") is not None else 0,
-                                 int(r["end"]) if r.get("end") else 65535) for r in rp.get("ranges") or ())
+        ranges = tuple(RangeSpec(int(r["begin"]) if r.get("begin") is not None else RangeSpec.MIN_PORT,
+                                 int(r["end"]) if r.get("end") else RangeSpec.MAX_PORT)
+                       for r in rp.get("ranges") or ())
         vip = rp.get("vip")
         if vip is None:
             spec = PortSpec(ranges=ranges, **common)

@@ -133,10 +133,8 @@ def test_port_ranges():
     assert (p[0].port_name, p[0].env_key) == ("name1", "key1")
     assert [(r.begin, r.end) for r in p[0].ranges] == [(1, 21), (2000, 5050)]
     assert p[1].port_name == "name2"
-    assert [(r.begin, r.end) for r in p[1].ranges] == [(S.RangeSpec.MIN_PORT if hasattr(S.RangeSpec, "MIN_PORT")
-                                                         else 0, 21),
-                                                        (5000, S.RangeSpec.MAX_PORT if hasattr(S.RangeSpec, "MAX_PORT")
-                                                         else 65535)]
+    # a missing begin is MIN_PORT, a missing end MAX_PORT (RangeSpec.java:26-27)
+    assert [(r.begin, r.end) for r in p[1].ranges] == [(S.RangeSpec.MIN_PORT, 21), (5000, S.RangeSpec.MAX_PORT)]
 
 
 def test_multiple_ports():
