@@ -257,24 +257,34 @@ class ResourceBuilder:
         raise ValueError(f"Unexpected disk type: {spec.type}")
 
     @staticmethod
+    def _existing_roles(resource: P.Resource):
+        """(role, pre-reserved role) of a resource we reserved. A legacy reservation (no
+        ``reservations`` stack) carries our role in ``resource.role``; the reference reads only
+        the stack and so rebuilds legacy resources as ``*`` (ResourceBuilder.java:139-161)."""
+        if len(resource.reservations) == 0 and resource.HasField("reservation"):
+            return resource.role or ANY_ROLE, ANY_ROLE
+        return get_role(resource), resource.role or ANY_ROLE
+
+    @staticmethod
     def from_existing_resource(resource: P.Resource) -> "ResourceBuilder":
+        role, pre_reserved_role = ResourceBuilder._existing_roles(resource)
         if not resource.HasField("disk"):
             if not has_resource_id(resource):
                 raise ValueError("Cannot generate resource spec from resource which has not been reserved by the SDK.")
-            spec = ResourceSpec(name=resource.name, value=V.get_value(resource), role=get_role(resource),
-                                principal=get_principal(resource) or "", pre_reserved_role=resource.role or ANY_ROLE)
+            spec = ResourceSpec(name=resource.name, value=V.get_value(resource), role=role,
+                                principal=get_principal(resource) or "", pre_reserved_role=pre_reserved_role)
             return ResourceBuilder.from_spec(spec, get_resource_id(resource), get_namespace(resource),
                                              get_framework_id(resource))
         disk = resource.disk
         if disk.HasField("source"):
             profiles = [disk.source.profile] if disk.source.HasField("profile") else []
-            spec = VolumeSpec(name=DISK_RESOURCE_TYPE, value=V.get_value(resource), role=get_role(resource),
-                              principal=disk.persistence.principal, pre_reserved_role=resource.role or ANY_ROLE,
+            spec = VolumeSpec(name=DISK_RESOURCE_TYPE, value=V.get_value(resource), role=role,
+                              principal=disk.persistence.principal, pre_reserved_role=pre_reserved_role,
                               type=VolumeType.MOUNT, container_path=disk.volume.container_path,
                               profiles=tuple(profiles))
         else:
-            spec = VolumeSpec(name=DISK_RESOURCE_TYPE, value=V.get_value(resource), role=get_role(resource),
-                              principal=disk.persistence.principal, pre_reserved_role=resource.role or ANY_ROLE,
+            spec = VolumeSpec(name=DISK_RESOURCE_TYPE, value=V.get_value(resource), role=role,
+                              principal=disk.persistence.principal, pre_reserved_role=pre_reserved_role,
                               type=VolumeType.ROOT, container_path=disk.volume.container_path)
         return ResourceBuilder.from_volume_spec(
             spec, get_resource_id(resource), get_namespace(resource), get_persistence_id(resource),
