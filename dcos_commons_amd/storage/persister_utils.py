@@ -48,6 +48,8 @@ def get_parent_paths(path: str) -> List[str]:
     """All ancestor paths of ``path`` (not itself), shallowest first; a leading slash is kept
     (PersisterUtils.getParentPaths: ``/a/b/c`` -> ``[/a, /a/b]``)."""
     elements = path.split(PATH_DELIM)
+    while elements and not elements[-1]:  # a trailing slash names no extra level
+        elements.pop()
     out, cur = [], ""
     for i in range(len(elements) - 1):
         if not elements[i]:
