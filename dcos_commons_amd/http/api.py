@@ -54,12 +54,51 @@ class Response:
             return self.body
         if isinstance(self.body, str):
             return self.body.encode("utf-8")
-        return json.dumps(self.body, indent=2).encode("utf-8")
+        return to_json_text(self.body).encode("utf-8")
 
     def json(self):
         if isinstance(self.body, (dict, list)):
             return self.body
         return json.loads(self.payload() or b"null")
+
+
+def to_json_text(value, indent: int = 2, _cur: int = 0) -> str:
+    """The layout of org.json's ``toString(2)`` that the reference's ResponseUtils writes: a
+    one-entry object or one-element array stays on one line, longer ones put each entry on its
+    own indented line (ResponseUtils.java jsonOkResponse)."""
+    if isinstance(value, dict):
+        if not value:
+            return "{}"
+        if len(value) == 1:
+            (k, v), = value.items()
+            return "{" + json.dumps(str(k)) + ": " + to_json_text(v, indent, _cur) + "}"
+        pad = _cur + indent
+        return "{\n" + ",\n".join(" " * pad + json.dumps(str(k)) + ": " + to_json_text(v, indent, pad)
+                                  for k, v in value.items()) + "\n" + " " * _cur + "}"
+    if isinstance(value, (list, tuple)):
+        if not value:
+            return "[]"
+        if len(value) == 1:
+            return "[" + to_json_text(value[0], indent, _cur) + "]"
+        pad = _cur + indent
+        return "[\n" + ",\n".join(" " * pad + to_json_text(v, indent, pad) for v in value) + "\n" + " " * _cur + "]"
+    return json.dumps(value)
+
+
+def read_data(stream, declared_size: Optional[int], size_limit: int) -> bytes:
+    """RequestUtils.readData: ``size_limit <= 0`` means unlimited. A declared size over the limit
+    fails before the stream is touched; the stream itself is read to at most one byte past the
+    limit, whatever size was declared."""
+    if stream is None:
+        raise ValueError("Missing payload")
+    if size_limit <= 0:
+        return stream.read()
+    if declared_size is not None and declared_size > size_limit:
+        raise ValueError(f"Stream exceeds {size_limit} byte size limit")
+    data = stream.read(size_limit + 1)
+    if len(data) > size_limit:
+        raise ValueError(f"Stream exceeds {size_limit} byte size limit")
+    return data
 
 
 def json_ok(body, status: int = 200) -> Response:

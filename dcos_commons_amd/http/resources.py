@@ -9,11 +9,12 @@ plan states to the reference's service status codes (HealthResource.java:31-88).
 """
 from __future__ import annotations
 
+import io
 import json
 import logging
 import re
 import uuid
-from typing import Dict, List, Optional
+from typing import Dict, List, Optional, Tuple
 
 from dcos_commons_amd import metrics, trace
 from dcos_commons_amd.debug import PlansTracker, TaskReservationsTracker, TaskStatusesTracker, thread_dump
@@ -29,6 +30,7 @@ from dcos_commons_amd.http.api import (
     json_ok,
     not_found,
     plain,
+    read_data,
     status_only,
 )
 from dcos_commons_amd.mesos import protos as P
@@ -61,6 +63,9 @@ def _pod_name(pod_type: str, index: int) -> str:
 
 
 def plan_info(plan) -> dict:
+    # the plan's status is read before its phases' (PlanInfo.forPlan): a phase that completes
+    # meanwhile shows COMPLETE under a plan still shown IN_PROGRESS, never the reverse
+    status = str(plan.get_status())
     return {
         "phases": [{
             "id": str(ph.get_id()),
@@ -72,7 +77,7 @@ def plan_info(plan) -> dict:
         } for ph in plan.get_children()],
         "errors": list(plan.get_errors()),
         "strategy": plan.get_strategy().get_name(),
-        "status": str(plan.get_status()),
+        "status": status,
     }
 
 
@@ -455,20 +460,23 @@ class ConfigResource:
             return status_only(500)
 
 
-def _parse_multipart_file(req: Request) -> bytes:
+def _parse_multipart_file(req: Request) -> Tuple[Optional[bytes], Optional[int]]:
+    """(file bytes, size declared in its Content-Disposition) of the ``file`` form field, or of the
+    raw body when the request is not multipart; (None, None) when there is no payload."""
     ctype = req.headers.get("Content-Type") or req.headers.get("content-type") or ""
     if "multipart/form-data" not in ctype:
-        return req.body
+        return (req.body or None), None
     m = re.search(r'boundary="?([^";]+)"?', ctype)
     if not m:
-        raise ValueError("Missing payload")
+        return None, None
     boundary = ("--" + m.group(1)).encode()
-    for part in req.body.split(boundary):
+    for part in (req.body or b"").split(boundary):
         if b'name="file"' not in part:
             continue
         head, _, data = part.partition(b"\r\n\r\n")
-        return data[:-2] if data.endswith(b"\r\n") else data
-    raise ValueError("Missing payload")
+        size = re.search(rb";\s*size=(-?\d+)", head)
+        return (data[:-2] if data.endswith(b"\r\n") else data), (int(size.group(1)) if size else None)
+    return None, None
 
 
 class StateResource:
@@ -512,11 +520,8 @@ class StateResource:
 
     def put_file(self, req: Request) -> Response:
         try:
-            data = _parse_multipart_file(req)
-            if not data and not req.body:
-                raise ValueError("Missing payload")
-            if len(data) > FILE_SIZE_LIMIT:
-                raise ValueError(f"Stream exceeds {FILE_SIZE_LIMIT} byte size limit")
+            data, declared = _parse_multipart_file(req)
+            data = read_data(io.BytesIO(data) if data is not None else None, declared, FILE_SIZE_LIMIT)
         except ValueError as e:
             return plain(str(e), 400)
         self.state_store.store_property(FILE_NAME_PREFIX + req.params["name"], data)
