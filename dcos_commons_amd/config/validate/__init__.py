@@ -235,16 +235,18 @@ class DomainCapabilityValidator(ConfigValidator):
         if capabilities.get_instance().supports_domains:
             return []
         errors = []
+        # (the reference formats this message with its two arguments swapped,
+        # DomainCapabilityValidator.java:37-52; here the pod type and the field are in place)
         tmpl = "The PlacementRule for PodSpec '%s' may not reference %s prior to DC/OS 1.11."
         for pod in new.pods:
             if pod.placement_rule is None:
                 continue
             if pl.references_zone(pod):
                 errors.append(ConfigValidationError.value_error("PlacementRule", str(pod.placement_rule),
-                                                                tmpl % ("Zones", pod.type)))
+                                                                tmpl % (pod.type, "Zones")))
             if pl.references_region(pod):
                 errors.append(ConfigValidationError.value_error("PlacementRule", str(pod.placement_rule),
-                                                                tmpl % ("Regions", pod.type)))
+                                                                tmpl % (pod.type, "Regions")))
         return errors
 
 
