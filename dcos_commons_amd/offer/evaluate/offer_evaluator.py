@@ -102,7 +102,17 @@ class OfferEvaluator:
         self.offer_outcome_tracker_v2 = offer_outcome_tracker_v2
         self.tls_stage_factory = tls_stage_factory
         self._framework_id: Optional[str] = None
+        self._executor_specs: Dict[tuple, List[ResourceSpec]] = {}
         self.logger = get_logger(__name__, resource_namespace)
+
+    def _executor_specs_for(self, role: str, principal: str, pre_reserved_role: str) -> List[ResourceSpec]:
+        """The executor's resource specs (immutable) for one role/principal, built once."""
+        key = (role, principal, pre_reserved_role)
+        specs = self._executor_specs.get(key)
+        if specs is None:
+            specs = self._executor_specs[key] = _executor_resource_specs(self.scheduler_config, role, principal,
+                                                                         pre_reserved_role)
+        return specs
 
     def _fid(self) -> P.FrameworkID:
         fid = self.framework_store.fetch_framework_id()
@@ -240,8 +250,7 @@ class OfferEvaluator:
             specs = _ordered_resource_specs(rs)
             if not added_executor:
                 added_executor = True
-                for spec in _executor_resource_specs(self.scheduler_config, specs[0].role, specs[0].principal,
-                                                     specs[0].pre_reserved_role):
+                for spec in self._executor_specs_for(specs[0].role, specs[0].principal, specs[0].pre_reserved_role):
                     stages.append(ResourceEvaluationStage(spec, [], None, ns, fid))
             if rs.id not in added_sets:
                 names = sorted(n for n, r in rs_by_task.items() if r.id == rs.id)
@@ -272,8 +281,7 @@ class OfferEvaluator:
             stages.append(PlacementRuleEvaluationStage(all_tasks, pod.placement_rule))
         first_spec = next(r for ts in pod.tasks for r in ts.resource_set.resources)
         mapper = ExecutorResourceMapper(
-            pod, _executor_resource_specs(self.scheduler_config, first_spec.role, first_spec.principal,
-                                          first_spec.pre_reserved_role),
+            pod, self._executor_specs_for(first_spec.role, first_spec.principal, first_spec.pre_reserved_role),
             executor_info.resources, ns, fid)
         for r in mapper.orphaned_resources:
             stages.append(DestroyEvaluationStage(r))

@@ -84,19 +84,22 @@ def evaluate_simple_resource(stage, spec: ResourceSpec, resource_id: Optional[st
         return ReserveEvaluationOutcome(EvaluationOutcome.fail(
             stage, "Offer lacks previously reserved '%s' with resourceId: '%s' for resource: '%s'",
             spec.name, resource_id, spec), None)
+    if resource_id is None:
+        # a new reservation: consume_reservable_merged hands out exactly the spec's value
+        b = ResourceBuilder.from_spec(spec, None, namespace, framework_id)
+        # an offered chunk that carried nothing beyond name/type/value builds to exactly what
+        # ResourceBuilder.from_spec(spec, new_id) produces, so it is built fresh and the task
+        # carries the same resource
+        plain = not (mr.resource.HasField("disk") or mr.resource.HasField("provider_id")
+                     or len(mr.resource.reservations) or mr.resource.HasField("reservation"))
+        resource = b.build() if plain else b.set_mesos_resource(mr).build()
+        rec = ReserveOfferRecommendation(pool.offer, resource)
+        new_id = b.built_resource_id
+        return ReserveEvaluationOutcome(EvaluationOutcome.pass_(
+            stage, "Offer contains sufficient unreserved '%s', generated new resourceId: '%s' "
+                   "for new reservation: '%s'", spec.name, new_id, spec,
+            recommendations=[rec], mesos_resource=mr), new_id, resource if plain else None)
     if V.equal(mr.value, spec.value):
-        if resource_id is None:
-            resource = ResourceBuilder.from_spec(spec, None, namespace, framework_id).set_mesos_resource(mr).build()
-            rec = ReserveOfferRecommendation(pool.offer, resource)
-            new_id = get_resource_id(resource)
-            # an offered chunk that carried nothing beyond name/type/value/(pre-)reservations builds
-            # to exactly what ResourceBuilder.from_spec(spec, new_id) would produce for the task
-            plain = not (mr.resource.HasField("disk") or mr.resource.HasField("provider_id")
-                         or len(mr.resource.reservations) or mr.resource.HasField("reservation"))
-            return ReserveEvaluationOutcome(EvaluationOutcome.pass_(
-                stage, "Offer contains sufficient unreserved '%s', generated new resourceId: '%s' "
-                       "for new reservation: '%s'", spec.name, new_id, spec,
-                recommendations=[rec], mesos_resource=mr), new_id, resource if plain else None)
         return ReserveEvaluationOutcome(EvaluationOutcome.pass_(
             stage, "Offer contains previously reserved '%s' with resourceId: '%s' for resource: '%s'",
             spec.name, resource_id, spec, mesos_resource=mr), resource_id)

@@ -44,7 +44,8 @@ class ReserveOfferRecommendation(OfferRecommendation):
     __slots__ = ()
 
     def __init__(self, offer: P.Offer, resource: P.Resource):
-        r = P.Resource()
+        op = Op(type=Op.RESERVE)
+        r = op.reserve.resources.add()  # copied once, straight into the operation
         r.CopyFrom(resource)
         if r.HasField("disk") and r.disk.HasField("source"):
             r.disk.ClearField("persistence")
@@ -52,8 +53,6 @@ class ReserveOfferRecommendation(OfferRecommendation):
         else:
             r.ClearField("disk")
         r.ClearField("revocable")
-        op = Op(type=Op.RESERVE)
-        op.reserve.resources.add().CopyFrom(r)
         super().__init__(offer, op)
 
 

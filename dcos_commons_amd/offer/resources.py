@@ -228,6 +228,7 @@ class ResourceBuilder:
         self.disk_source = None
         self.mesos_resource: Optional[MesosResource] = None
         self.framework_id: Optional[str] = None
+        self.built_resource_id: Optional[str] = None  # the id ``build`` wrote into the reservation
 
     @staticmethod
     def from_spec(spec: ResourceSpec, resource_id: Optional[str] = None, resource_namespace: Optional[str] = None,
@@ -322,14 +323,15 @@ class ResourceBuilder:
         return self
 
     def _reservation_labels(self, labels: P.Labels) -> None:
-        """resource_id / framework_id / namespace labels, in the key order ``map_to_labels`` writes."""
-        kv = {L.RESOURCE_ID_RESERVATION_LABEL: self.resource_id or uuid4_str()}
+        """resource_id / framework_id / namespace labels, in the key order ``map_to_labels`` writes
+        (sorted: framework_id < namespace < resource_id)."""
+        rid = self.resource_id or uuid4_str()
+        self.built_resource_id = rid
         if self.framework_id is not None:
-            kv[L.FRAMEWORK_ID_RESERVATION_LABEL] = self.framework_id
+            labels.labels.add(key=L.FRAMEWORK_ID_RESERVATION_LABEL, value=self.framework_id)
         if self.resource_namespace is not None:
-            kv[L.NAMESPACE_RESERVATION_LABEL] = self.resource_namespace
-        for k in sorted(kv):
-            labels.labels.add(key=k, value=kv[k])
+            labels.labels.add(key=L.NAMESPACE_RESERVATION_LABEL, value=self.resource_namespace)
+        labels.labels.add(key=L.RESOURCE_ID_RESERVATION_LABEL, value=rid)
 
     def _reservation(self) -> P.Resource.ReservationInfo:
         r = P.Resource.ReservationInfo(role=self.role, type=P.Resource.ReservationInfo.DYNAMIC,

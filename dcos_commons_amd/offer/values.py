@@ -146,6 +146,9 @@ def sufficient(desired, available) -> bool:
         return True
     if available is None:
         return False
+    if desired.type == P.Value.SCALAR and available.type == P.Value.SCALAR:
+        # the common case (cpus/mem/disk/gpus) without building intermediate Value protos
+        return fixed(desired.scalar.value - available.scalar.value) <= 0
     return compare(subtract(desired, available), get_zero(desired.type)) <= 0
 
 
