@@ -19,6 +19,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)
 OPS = os.path.join(ROOT, "dcos_commons_amd", "ops")
 NATIVE = os.path.join(ROOT, "native")
 BUILD = os.path.join(NATIVE, "build")
+BUILD_SANITIZE = os.path.join(NATIVE, "build-sanitize")  # ASan/UBSan host tools (tests only)
 ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950").split(";")[0] or "gfx950"
 
 
@@ -63,20 +64,30 @@ def build_probe_binary(force: bool = False, verbose: bool = False) -> str:
     return out
 
 
-def build_cpp_tools(force: bool = False, verbose: bool = False) -> List[str]:
-    """CMake build of the C++ natives (bootstrap, CLI, TLS crypto library) if their sources exist."""
+def build_cpp_tools(force: bool = False, verbose: bool = False, sanitize: bool = False) -> List[str]:
+    """CMake build of the C++ natives (bootstrap, CLI, TLS crypto library) if their sources exist.
+
+    ``sanitize=True`` builds the host tools (bootstrap, CLI, unit tests) with AddressSanitizer and
+    UBSan into ``native/build-sanitize``; it is a CPU-only build, never shipped."""
     if not os.path.exists(os.path.join(NATIVE, "CMakeLists.txt")):
         return []
-    os.makedirs(BUILD, exist_ok=True)
-    targets = [os.path.join(BUILD, n) for n in ("sdk-bootstrap", "sdk-cli", "native-tests", "libsdktls.so")]
+    out = BUILD_SANITIZE if sanitize else BUILD
+    os.makedirs(out, exist_ok=True)
+    names = ("sdk-bootstrap", "sdk-cli", "native-tests") + (() if sanitize else ("libsdktls.so",))
+    targets = [os.path.join(out, n) for n in names]
     srcs = []
     for d, _, fs in os.walk(NATIVE):
-        if os.path.abspath(d).startswith(os.path.abspath(BUILD)):
+        if os.path.abspath(d).startswith((os.path.abspath(BUILD), os.path.abspath(BUILD_SANITIZE))):
             continue
         srcs.extend(os.path.join(d, f) for f in fs if f.endswith((".cpp", ".h", ".hpp", ".txt")))
     if force or any(_stale(t, srcs) for t in targets):
-        _run(["cmake", "-S", NATIVE, "-B", BUILD, "-DCMAKE_BUILD_TYPE=Release", "-G", "Ninja"], verbose)
-        _run(["cmake", "--build", BUILD, "-j", "8"], verbose)
+        if sanitize:
+            _run(["cmake", "-S", NATIVE, "-B", out, "-DCMAKE_BUILD_TYPE=Debug", "-DSDK_SANITIZE=ON", "-G", "Ninja"],
+                 verbose)
+            _run(["cmake", "--build", out, "-j", "8", "--target", *names], verbose)
+        else:
+            _run(["cmake", "-S", NATIVE, "-B", out, "-DCMAKE_BUILD_TYPE=Release", "-G", "Ninja"], verbose)
+            _run(["cmake", "--build", out, "-j", "8"], verbose)
     return targets
 
 

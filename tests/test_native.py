@@ -11,16 +11,32 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 BUILD = os.path.join(ROOT, "native", "build")
 
 
-@pytest.fixture(scope="module")
-def tools():
+# Every native test runs against the release build and against an AddressSanitizer + UBSan build
+# of the same sources (the reference has no native code, so no sanitizers; the C++
+# natives here get them). Sanitizer findings abort the tool, which fails the test.
+SANITIZER_ENV = {"ASAN_OPTIONS": "halt_on_error=1:abort_on_error=1:detect_leaks=1",
+                 "UBSAN_OPTIONS": "halt_on_error=1:print_stacktrace=1"}
+
+
+@pytest.fixture(scope="module", params=["release", "sanitize"])
+def tools(request):
     sys.path.insert(0, ROOT)
     from dcos_commons_amd.ops import build
 
+    sanitize = request.param == "sanitize"
     try:
-        build.build_cpp_tools()
+        targets = build.build_cpp_tools(sanitize=sanitize)
     except Exception as e:  # noqa: BLE001
         pytest.skip(f"native toolchain unavailable: {e}")
-    return {n: os.path.join(BUILD, n) for n in ("sdk-bootstrap", "sdk-cli", "native-tests")}
+    saved = {k: os.environ.get(k) for k in SANITIZER_ENV}
+    if sanitize:
+        os.environ.update(SANITIZER_ENV)
+    yield {os.path.basename(t): t for t in targets}
+    for k, v in saved.items():
+        if v is None:
+            os.environ.pop(k, None)
+        else:
+            os.environ[k] = v
 
 
 def test_native_unit_tests(tools):
