@@ -73,7 +73,7 @@ def build_cpp_tools(force: bool = False, verbose: bool = False, sanitize: bool =
         return []
     out = BUILD_SANITIZE if sanitize else BUILD
     os.makedirs(out, exist_ok=True)
-    names = ("sdk-bootstrap", "sdk-cli", "native-tests") + (() if sanitize else ("libsdktls.so",))
+    names = ("sdk-bootstrap", "sdk-cli", "native-tests", "tls-tests") + (() if sanitize else ("libsdktls.so",))
     targets = [os.path.join(out, n) for n in names]
     srcs = []
     for d, _, fs in os.walk(NATIVE):

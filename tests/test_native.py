@@ -44,6 +44,13 @@ def test_native_unit_tests(tools):
     assert r.returncode == 0, r.stdout + r.stderr
 
 
+def test_tls_library_round_trips(tools):
+    """Keys, CSRs, root/intermediate CAs, chain checks, PKCS#12 stores, RS256/JWT and error paths
+    of the TLS crypto code (native/tests/test_tls.cpp), instrumented in the sanitizer build."""
+    r = subprocess.run([tools["tls-tests"]], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and "tls tests passed" in r.stdout, r.stdout + r.stderr
+
+
 def test_bootstrap_renders_config_templates(tools, tmp_path):
     sandbox = tmp_path
     (sandbox / "tpl.conf").write_text("name={{NAME}}\n{{#FLAG}}flag on\n{{/FLAG}}{{^OFF}}off is off\n{{/OFF}}"
