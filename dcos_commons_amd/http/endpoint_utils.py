@@ -55,8 +55,13 @@ def to_vip_endpoint(service_name: str, scheduler_config, vip_name: str, vip_port
 
 
 def template_url_factory(service_name: str, scheduler_config, prefix: str = ""):
-    """ArtifactResource.getUrlFactory: task config templates are served by the scheduler."""
+    """ArtifactResource.getUrlFactory: task config templates are served by the scheduler. With a
+    ``prefix`` (the service's name in a multi-service scheduler) the URL goes through
+    ``/v1/service/<sanitized prefix>``, slashes becoming dots (MultiArtifactResource.getUrlFactory)."""
+    from dcos_commons_amd.offer.common_id_utils import to_sanitized_service_name
+
     host_port = to_scheduler_auto_ip_endpoint(service_name, scheduler_config)
+    prefix = to_sanitized_service_name(prefix) if prefix else ""
 
     def factory(config_id, pod_type: str, task_name: str, config_name: str) -> str:
         if prefix:

@@ -483,7 +483,9 @@ class StateResource:
     def __init__(self, framework_store, state_store, property_deserializer=None):
         self.framework_store = framework_store
         self.state_store = state_store
-        self.deserialize = property_deserializer or (lambda key, value: value.decode("utf-8"))
+        from dcos_commons_amd.state.serializer import StringPropertyDeserializer
+
+        self.deserialize = property_deserializer or StringPropertyDeserializer()
 
     def routes(self) -> List[Route]:
         return [

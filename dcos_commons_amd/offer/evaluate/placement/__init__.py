@@ -448,14 +448,24 @@ class AttributeRule(_StringMatcherRule):
 
 
 class RuleFactory:
+    """``require``/``avoid`` take one matcher, several, or one collection of them; several become
+    an OrRule (negated for ``avoid``) (RuleFactory.java defaults, PlacementUtils.require)."""
+
     def __init__(self, cls):
         self.cls = cls
 
-    def require(self, matcher: StringMatcher) -> PlacementRule:
-        return self.cls(matcher)
+    @staticmethod
+    def _matchers(matchers) -> List[StringMatcher]:
+        if len(matchers) == 1 and not isinstance(matchers[0], StringMatcher):
+            return list(matchers[0])
+        return list(matchers)
 
-    def avoid(self, matcher: StringMatcher) -> PlacementRule:
-        return NotRule(self.cls(matcher))
+    def require(self, *matchers) -> PlacementRule:
+        ms = self._matchers(matchers)
+        return self.cls(ms[0]) if len(ms) == 1 else OrRule([self.cls(m) for m in ms])
+
+    def avoid(self, *matchers) -> PlacementRule:
+        return NotRule(self.require(*matchers))
 
 
 HostnameRuleFactory = RuleFactory(HostnameRule)

@@ -302,6 +302,28 @@ class NamedVIPSpec(PortSpec):
                 f"vip={self.vip_name}:{self.vip_port})")
 
 
+@dataclass(frozen=True)
+class VipSpec:
+    """DefaultVipSpec: an application port published under a VIP name and port (both ports
+    non-negative, the name non-empty; reference specification/DefaultVipSpec.java)."""
+
+    application_port: int
+    vip_name: str
+    vip_port: int
+
+    def __post_init__(self):
+        _require(self.application_port >= 0, "applicationPort must be non-negative")
+        _require(bool(self.vip_name), "vipName must be non-empty")
+        _require(self.vip_port >= 0, "vipPort must be non-negative")
+
+    def to_dict(self):
+        return {"application-port": self.application_port, "vip-name": self.vip_name, "vip-port": self.vip_port}
+
+    @staticmethod
+    def from_dict(d: Dict[str, Any]) -> "VipSpec":
+        return VipSpec(int(d["application-port"]), d["vip-name"], int(d["vip-port"]))
+
+
 def resource_spec_from_dict(d: Dict[str, Any]) -> ResourceSpec:
     t = d.get("@type", "DefaultResourceSpec")
     common = dict(

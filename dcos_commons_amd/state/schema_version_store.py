@@ -28,10 +28,13 @@ class SchemaVersionStore:
         self.persister = persister
 
     def check(self, expected: SchemaVersion) -> None:
+        """ValueError (the reference's IllegalArgumentException) unless the stored version is
+        ``expected``; an unknown number is reported as stored."""
         cur = self.get_or_set_version(expected)
         if cur != expected:
-            raise RuntimeError(
-                f"Storage schema version {cur.value} is not supported by this software (expected: {expected.value})")
+            shown = self.persister.get(SCHEMA_VERSION_NAME).decode() if cur == SchemaVersion.UNKNOWN else cur.value
+            raise ValueError(
+                f"Storage schema version {shown} is not supported by this software (expected: {expected.value})")
 
     def get_or_set_version(self, expected: SchemaVersion) -> SchemaVersion:
         try:

@@ -4,7 +4,6 @@ Reference: sdk/.../state/StateStoreUtils.java:38-256.
 """
 from __future__ import annotations
 
-import json
 import logging
 from typing import List, Optional
 
@@ -12,6 +11,7 @@ from dcos_commons_amd.mesos import protos as P
 from dcos_commons_amd.offer import common_id_utils
 from dcos_commons_amd.storage.persister import Reason
 
+from .serializer import JsonSerializer
 from .state_store import StateStore, StateStoreException
 
 LOGGER = logging.getLogger(__name__)
@@ -87,7 +87,7 @@ def _fetch_bool(store: StateStore, key: str) -> bool:
     if not data:
         return False
     try:
-        return bool(json.loads(data.decode()))
+        return bool(JsonSerializer().deserialize(data))
     except ValueError as e:
         raise StateStoreException(Reason.SERIALIZATION_ERROR, str(e)) from e
 
@@ -97,7 +97,7 @@ def is_uninstalling(store: StateStore) -> bool:
 
 
 def set_uninstalling(store: StateStore) -> None:
-    store.store_property(UNINSTALLING_PROPERTY_KEY, b"true")
+    store.store_property(UNINSTALLING_PROPERTY_KEY, JsonSerializer().serialize(True))
 
 
 def store_task_status_as_property(store: StateStore, task_name: str, status: P.TaskStatus) -> None:

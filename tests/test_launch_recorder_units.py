@@ -138,7 +138,7 @@ def test_schema_version_auto_initializes_and_round_trips():
     assert p.get("SchemaVersion") == b"1"
     s.store(SchemaVersion.MULTI_SERVICE)
     assert SchemaVersionStore(p).get_or_set_version(SchemaVersion.SINGLE_SERVICE) == SchemaVersion.MULTI_SERVICE
-    with pytest.raises(RuntimeError):
+    with pytest.raises(ValueError, match="version 2 is not supported"):
         SchemaVersionStore(p).check(SchemaVersion.SINGLE_SERVICE)
 
 
