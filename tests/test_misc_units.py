@@ -5,7 +5,7 @@ check, the multi-service schema check, and step state across a scheduler restart
 
 Mirrors sdk/scheduler/src/test/java/com/mesosphere/sdk/{specification/yaml/WriteOnceLinkedHashMapTest,
 http/types/StringPropertyDeserializerTest, state/JsonSerializerTest, specification/DefaultVipSpecTest,
-http/endpoints/MultiArtifactResourceTest, offer/evaluate/placement/{AgentRuleTest,HostnameRuleTest,
+http/endpoints/{ArtifactResourceTest,MultiArtifactResourceTest}, offer/evaluate/placement/{AgentRuleTest,HostnameRuleTest,
 ZoneRuleTest,RegionRuleTest,InvalidPlacementRuleTest}, specification/validation/ZoneValidatorTest,
 config/validate/TaskEnvCannotChangeTest, framework/ApiServerTest, scheduler/multi/MultiServiceRunnerTest}.java
 and frameworks/helloworld/.../SchedulerRestartServiceTest.java.
@@ -74,6 +74,15 @@ def test_vip_spec():
 # multi-service template URLs
 
 ARTIFACT_CFG = SchedulerConfig.for_testing(PORT_API=1234, SERVICE_TLD="some.tld", MARATHON_NAME="test-marathon")
+
+
+@pytest.mark.parametrize("service,host", [("svc-name", "svc-name"), ("/path/to/svc-name", "svc-name-to-path")])
+def test_standalone_template_url(service, host):
+    """ArtifactResourceTest: a single service's templates come from its own /v1/artifacts."""
+    config_id = uuid.uuid4()
+    url = endpoint_utils.template_url_factory(service, ARTIFACT_CFG)(config_id, "some-pod", "some-task", "some-config")
+    assert url == (f"http://{host}.test-marathon.some.tld:1234/v1/artifacts/template/"
+                   f"{config_id}/some-pod/some-task/some-config")
 
 
 @pytest.mark.parametrize("framework,service,host,path", [
