@@ -14,6 +14,7 @@ rules.
 from __future__ import annotations
 
 import logging
+import sys
 from typing import Callable, Optional, Set
 
 from dcos_commons_amd.dcos import capabilities as caps
@@ -92,6 +93,9 @@ class FrameworkRunner:
             self._run_skeleton_scheduler(block)
             ProcessExit.exit(ProcessExit.DRIVER_EXITED)
             return None
+        switch_s = self.scheduler_config.gil_switch_interval_s()
+        if switch_s > 0:
+            sys.setswitchinterval(switch_s)
         framework_store = FrameworkStore(persister)
         self.framework_scheduler = FrameworkScheduler(self.resource_roles(), self.scheduler_config, persister,
                                                       framework_store, client)

@@ -222,6 +222,10 @@ class DefaultScheduler(AbstractScheduler):
         return OfferResponse.processed(self.plan_scheduler.resource_offers(offers, steps, on_step), streamed=True)
 
     def get_unexpected_resources(self, unused_offers) -> UnexpectedResourcesResponse:
+        if not any(get_resource_id(r) is not None for offer in unused_offers for r in offer.resources):
+            # nothing reserved by this SDK in the leftover offers: no need to load every task to
+            # learn which reservations are still expected
+            return UnexpectedResourcesResponse.processed([])
         try:
             keep = set()
             for t in self.state_store.fetch_tasks():

@@ -147,9 +147,12 @@ class DefaultRecoveryPlanManager(PlanManager):
         self._lock = threading.RLock()
         self.logger = get_logger(__name__, namespace)
 
+    # ``_plan`` is replaced wholesale (one atomic attribute store) and never mutated in place, so
+    # readers and status updates take the current plan without the lock: a status arriving while
+    # the offer loop regenerates the plan must not wait for that regeneration. The steps a new
+    # plan carries over are the same objects, so an update applied to the outgoing plan lands.
     def get_plan(self):
-        with self._lock:
-            return self._plan
+        return self._plan
 
     def set_plan(self, plan) -> None:
         raise NotImplementedError("Setting plans on the RecoveryPlanManager is not allowed.")
@@ -164,8 +167,7 @@ class DefaultRecoveryPlanManager(PlanManager):
             return self._plan.get_candidates(dirty_assets)
 
     def update(self, status) -> None:
-        with self._lock:
-            self._plan.update(status)
+        self._plan.update(status)
 
     def get_dirty_assets(self):
         return get_dirty_assets(self._plan)
