@@ -43,7 +43,8 @@ PROFILES = {
                   "SDK_REVIVE_INTERVAL_S": "5", "SDK_REVIVE_BURST_INTERVAL_S": "5",
                   "SDK_RESERVATION_GC_ALL_OFFERS": "false",
                   "SDK_FAST_UNSUPPRESS": "false", "SDK_MERGE_AGENT_OFFERS": "false",
-                  "SDK_LAUNCH_RECONCILE_S": "0", "SDK_UNKNOWN_AS_LOST": "false", "SDK_STREAM_LAUNCHES": "false"},
+                  "SDK_LAUNCH_RECONCILE_S": "0", "SDK_UNKNOWN_AS_LOST": "false", "SDK_STREAM_LAUNCHES": "false",
+                  "SDK_REVIVE_ONLY_UNMATCHED": "false"},
 }
 
 
@@ -83,14 +84,23 @@ class DeployBench:
         self.agent_runners = agent_runners  # per-agent check runner (remote GPU agents)
 
     # -- helpers ---------------------------------------------------------------------------
-    def _wait(self, pred, what: str) -> float:
+    def _wait(self, pred, what: str, event=None) -> float:
+        """Until ``pred()``. With ``event`` (the scheduler's status-processed event) the predicate
+        is re-checked whenever a status has been processed (and every 5 ms regardless), so the
+        observer neither lags the completing status by a poll period nor competes with the
+        scheduler for the interpreter between statuses."""
         t0 = time.perf_counter()
         while True:
+            if event is not None:
+                event.clear()
             if pred():
                 return time.perf_counter() - t0
             if time.perf_counter() - t0 > self.timeout_s:
                 raise TimeoutError(f"timed out after {self.timeout_s}s waiting for {what}")
-            time.sleep(0.001)
+            if event is not None:
+                event.wait(0.005)
+            else:
+                time.sleep(0.001)
 
     @staticmethod
     def _plan_done(scheduler, name: str) -> bool:
@@ -150,7 +160,8 @@ class DeployBench:
             router = runner.framework_runner.api_server.router
             state_store = runner.scheduler.state_store
             sched = runner.scheduler
-            self._wait(lambda: self._plan_done(sched, "deploy"), "deploy plan COMPLETE")
+            ev = sched.status_processed
+            self._wait(lambda: self._plan_done(sched, "deploy"), "deploy plan COMPLETE", ev)
             deploy_s = time.perf_counter() - t0
             self._expect_api(router, "deploy")
 
@@ -164,7 +175,7 @@ class DeployBench:
             t1 = time.perf_counter()
             master.fail_task(old)
             self._wait(lambda: self._pod_ready(state_store, "hello-0-server", old) and
-                       self._plan_done(sched, "recovery"), "restart recovery")
+                       self._plan_done(sched, "recovery"), "restart recovery", ev)
             mttr_restart = time.perf_counter() - t1
             self._expect_api(router, "recovery")
 
@@ -177,7 +188,7 @@ class DeployBench:
             if r.status != 200:
                 raise RuntimeError(f"replace failed: {r.status} {r.payload()!r}")
             self._wait(lambda: self._pod_ready(state_store, "hello-0-server", old) and
-                       self._plan_done(sched, "recovery"), "replace recovery")
+                       self._plan_done(sched, "recovery"), "replace recovery", ev)
             mttr_replace = time.perf_counter() - t2
             self._expect_api(router, "recovery")
         finally:

@@ -25,6 +25,24 @@ from .process_exit import ProcessExit
 
 LOGGER = logging.getLogger(__name__)
 
+_NO_NEW_WORK_STATES = (P.TASK_STAGING, P.TASK_STARTING)
+
+
+def can_create_work(status: P.TaskStatus) -> bool:
+    """Whether a status can give the plans new work, i.e. whether it is worth waking the offer loop.
+
+    A task moving through STAGING / STARTING, or RUNNING while its readiness check has not
+    reported yet, only advances a step that is already launched (STARTING -> STARTED): no step
+    becomes a candidate and nothing becomes idle, so an offer cycle run for it would find nothing
+    to do while holding the interpreter that the pending check result needs. Everything else
+    (readiness results, RUNNING without a check, terminal and unreachable states) wakes it."""
+    if status.state in _NO_NEW_WORK_STATES:
+        return False
+    if status.state == P.TASK_RUNNING and status.HasField("check_status") and \
+            status.check_status.HasField("command"):
+        return status.check_status.command.HasField("exit_code")   # absent: the check is still pending
+    return True
+
 
 class FrameworkScheduler:
     def __init__(self, roles_whitelist, scheduler_config, persister, framework_store, client,
@@ -42,7 +60,8 @@ class FrameworkScheduler:
             gc_all_offers=scheduler_config.is_reservation_gc_on_all_offers() if scheduler_config is not None else False,
             fast_unsuppress=scheduler_config.is_fast_unsuppress() if scheduler_config is not None else False,
             merge_agent_offers=scheduler_config.is_merge_agent_offers() if scheduler_config is not None else False,
-            stream_launches=scheduler_config.is_stream_launches() if scheduler_config is not None else False)
+            stream_launches=scheduler_config.is_stream_launches() if scheduler_config is not None else False,
+            revive_only_unmatched=scheduler_config.is_revive_only_unmatched() if scheduler_config is not None else False)
         if implicit_reconciler is None:
             implicit_reconciler = ImplicitReconciler(
                 scheduler_config.implicit_reconcile_delay_s() if scheduler_config is not None else 0.0,
@@ -146,7 +165,8 @@ class FrameworkScheduler:
                 else:
                     LOGGER.warning("Received status update for unknown task, but task should not be killed "
                                    "again: %s", status.task_id.value)
-            self.offer_processor.kick()
+            if resp.result == TaskStatusResult.UNKNOWN_TASK or can_create_work(status):
+                self.offer_processor.kick()
         except Exception as e:  # noqa: BLE001
             self._exit(e)
 

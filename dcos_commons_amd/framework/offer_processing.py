@@ -215,6 +215,11 @@ class ReviveManager:
             self._revive_bypass = True
         self.revive_requested = True
 
+    def cancel_request(self) -> None:
+        """The work that asked for a revive was matched with offers already in hand."""
+        self.revive_requested = False
+        self._revive_bypass = False
+
     def revive_if_requested(self) -> None:
         if not self.revive_requested:
             return
@@ -414,7 +419,8 @@ class OfferProcessor:
     def __init__(self, client, persister, scheduler_config=None, token_bucket: Optional[TokenBucket] = None,
                  queue_capacity: int = DEFAULT_QUEUE_CAPACITY, offer_wait_s: Optional[float] = None,
                  hold_s: float = 0.0, event_driven: bool = False, gc_all_offers: bool = False,
-                 fast_unsuppress: bool = False, merge_agent_offers: bool = False, stream_launches: bool = False):
+                 fast_unsuppress: bool = False, merge_agent_offers: bool = False, stream_launches: bool = False,
+                 revive_only_unmatched: bool = False):
         self.client = client
         self.persister = persister
         self.offer_wait_s = offer_wait_s if offer_wait_s is not None else (
@@ -434,6 +440,8 @@ class OfferProcessor:
         self.merge_agent_offers = merge_agent_offers
         # ACCEPT each step's launch as soon as it is matched instead of after the whole cycle
         self.stream_launches = stream_launches
+        # drop a revive requested for new work when that work was matched in the same cycle
+        self.revive_only_unmatched = revive_only_unmatched
         # (real) offer id -> (offer, hold deadline). Rescinds arrive on the driver's thread while
         # the offer thread evaluates, so the map is only touched under _held_lock, and an offer
         # rescinded mid-cycle is remembered so that the cycle does not hold it again.
@@ -547,6 +555,11 @@ class OfferProcessor:
                 if self._check_status():
                     self._evaluate(offers, now)
                     sp.set(working=True)
+                    if self.revive_only_unmatched and self.revive_manager.revive_requested and \
+                            self._candidates_all_launched():
+                        # the new work was matched in this very cycle: asking the master for more
+                        # offers would only bring back this cycle's leftovers for another pass
+                        self.revive_manager.cancel_request()
                     if getattr(self.client, "consume_recheck_request", None) is not None and \
                             self.client.consume_recheck_request():
                         # the client started work that changes its status (e.g. uninstall's
@@ -569,6 +582,12 @@ class OfferProcessor:
             with self._in_progress_lock:
                 for o in new_offers:
                     self._in_progress.discard(o.id.value)
+
+    def _candidates_all_launched(self) -> bool:
+        steps = getattr(self.client, "candidate_steps", None)
+        if not steps:
+            return False
+        return not any(s.is_pending() or s.is_prepared() for s in steps)
 
     def _check_status(self) -> bool:
         resp = self.client.get_client_status()

@@ -45,6 +45,7 @@ from dcos_commons_amd.mesos.resource_math import (
     pop_reservation,
     strip_volume,
 )
+from dcos_commons_amd import trace
 from dcos_commons_amd.utils import ids
 
 LOGGER = logging.getLogger(__name__)
@@ -870,12 +871,14 @@ class LocalMaster:
     def _run_check(self, task: _Task, epoch: int) -> None:
         if task.epoch != epoch or task.status.state != P.TASK_RUNNING:
             return
+        trace.instant("check_submit", "master", task=task.info.name)
         runner = self._check_runner(task)
         devices = list(task.gpu_devices)
 
         def work():
             try:
-                ok = bool(runner(task.info, devices))
+                with trace.span("readiness_check", "master", task=task.info.name):
+                    ok = bool(runner(task.info, devices))
             except Exception:  # noqa: BLE001
                 LOGGER.exception("check of %s raised", task.info.name)
                 ok = False
@@ -898,6 +901,7 @@ class LocalMaster:
     def _lifecycle_ready(self, task: _Task, epoch: int) -> None:
         if task.epoch != epoch or task.status.state != P.TASK_RUNNING:
             return
+        trace.instant("task_ready", "master", task=task.info.name)
         cs = P.CheckStatusInfo(type=task.info.check.type)
         cs.command.exit_code = 0
         extra = {"check_status": cs, "reason": P.TaskStatus.REASON_TASK_CHECK_STATUS_UPDATED}

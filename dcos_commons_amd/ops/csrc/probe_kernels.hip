@@ -454,4 +454,155 @@ void pattern_check_kernel(const uint4* __restrict__ p, size_t n16, uint32_t seed
   if ((threadIdx.x & 63) == 0 && bad) atomicAdd(errors, (unsigned long long)bad);
 }
 
+// ---------------------------------------------------------------------------------------
+// Fused readiness check. A pod's readiness probe is on the deploy / recovery critical path, so
+// it runs as ONE host call: five launches back to back on a private stream and a single 32-byte
+// read-back, instead of a chain of framework ops with a host sync in the middle.
+//   readiness_prep_kernel  A, Bt <- hashed bf16 operands, X <- hashed fp32 vectors, result <- 0
+//   gemm (MFMA)            C = A Bt^T
+//   freivalds_kernel       ||C X - A (Bt^T X)||^2 and ||A (Bt^T X)||^2 (Freivalds' check:
+//                          O(MN + NK + MK) work instead of a second GEMM)
+//   pattern_write/check    address-hashed write + verify over a 64 MiB buffer
+// ---------------------------------------------------------------------------------------
+struct ReadinessResult {
+  float diff2;                  // sum over (m, v) of (C X - A (Bt^T X))^2
+  float want2;                  // sum over (m, v) of (A (Bt^T X))^2
+  unsigned long long bad_words;
+  unsigned long long reserved;
+};
+
+constexpr int FV = 4;           // Freivalds vectors
+constexpr int FREIVALDS_THREADS = 1024;
+constexpr int FREIVALDS_MAX_K = 4096;
+
+__device__ __forceinline__ float hashed_unit(uint64_t i, uint32_t seed) {
+  // uniform in [-1, 1) from the top 24 bits of the hash
+  return (float)(mix32((i << 2) ^ ((uint64_t)(seed ^ 0x9E3779B9u) << 40)) >> 8) * (2.0f / 16777216.0f) - 1.0f;
+}
+
+__global__ __launch_bounds__(256)
+void readiness_prep_kernel(uint4* __restrict__ ab, size_t ab16, float* __restrict__ x, int nx, uint32_t seed,
+                           ReadinessResult* __restrict__ res) {
+  const size_t tid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  for (size_t i = tid; i < ab16; i += stride) {
+    const uint64_t base = (i << 2) ^ ((uint64_t)seed << 40);
+    uint4 v = make_uint4(mix32(base), mix32(base + 1), mix32(base + 2), mix32(base + 3));
+    // finite bf16 pairs: random sign and mantissa, |x| in [0.5, 1)
+    v.x = (v.x & 0x807F807Fu) | 0x3F003F00u;
+    v.y = (v.y & 0x807F807Fu) | 0x3F003F00u;
+    v.z = (v.z & 0x807F807Fu) | 0x3F003F00u;
+    v.w = (v.w & 0x807F807Fu) | 0x3F003F00u;
+    ab[i] = v;
+  }
+  for (size_t i = tid; i < (size_t)nx; i += stride) x[i] = hashed_unit(i, seed);
+  if (tid == 0) {
+    res->diff2 = 0.f;
+    res->want2 = 0.f;
+    res->bad_words = 0ull;
+    res->reserved = 0ull;
+  }
+}
+
+// One workgroup of 16 waves. X is N x FV (row-major), C is M x N fp32, A is M x K and Bt is N x K
+// bf16 (K-contiguous). Requires N % 4 == 0, K % 8 == 0, K <= FREIVALDS_MAX_K (host-checked).
+// `inject` = 1 reads C[0:16][0:16] as zeros, a lost MFMA tile (tests that the check catches it).
+__global__ __launch_bounds__(FREIVALDS_THREADS)
+void freivalds_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, const float* __restrict__ C,
+                      const float* __restrict__ X, int M, int N, int K, int inject, float* __restrict__ out2) {
+  __shared__ float y[FREIVALDS_MAX_K * FV];   // y = Bt^T X   (K x FV)
+  __shared__ float red[2][FREIVALDS_THREADS / 64];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  constexpr int NW = FREIVALDS_THREADS / 64;
+  for (int i = tid; i < K * FV; i += FREIVALDS_THREADS) y[i] = 0.f;
+  __syncthreads();
+
+  // phase 1: wave w sums rows n = w, w + 16, ... of Bt; each lane owns 8 consecutive k per chunk
+  // (one 16-B load per row), partial sums merged with LDS atomics
+  const int kchunks = K / 8;
+  for (int kc = lane; kc < kchunks; kc += 64) {
+    float s[8][FV];
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+      for (int v = 0; v < FV; ++v) s[j][v] = 0.f;
+#pragma unroll 4
+    for (int n = wave; n < N; n += NW) {
+      const bf16x8 b = *reinterpret_cast<const bf16x8*>(Bt + (size_t)n * K + kc * 8);
+      const float4 xv = *reinterpret_cast<const float4*>(X + (size_t)n * FV);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float bj = (float)b[j];
+        s[j][0] += bj * xv.x;
+        s[j][1] += bj * xv.y;
+        s[j][2] += bj * xv.z;
+        s[j][3] += bj * xv.w;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+      for (int v = 0; v < FV; ++v) atomicAdd(&y[(kc * 8 + j) * FV + v], s[j][v]);
+  }
+  __syncthreads();
+
+  // phase 2: one wave per row m: got = C[m, :] X, want = A[m, :] y, reduced across the wave
+  float d2 = 0.f, w2 = 0.f;
+  const int nchunks = N / 4;
+  for (int m = wave; m < M; m += NW) {
+    float got[FV] = {0.f, 0.f, 0.f, 0.f}, want[FV] = {0.f, 0.f, 0.f, 0.f};
+    for (int nc = lane; nc < nchunks; nc += 64) {
+      float4 c = *reinterpret_cast<const float4*>(C + (size_t)m * N + nc * 4);
+      if (inject == 1 && m < 16 && nc < 4) c = make_float4(0.f, 0.f, 0.f, 0.f);   // a lost 16x16 tile
+      const float cv[4] = {c.x, c.y, c.z, c.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float4 xv = *reinterpret_cast<const float4*>(X + (size_t)(nc * 4 + j) * FV);
+        got[0] += cv[j] * xv.x;
+        got[1] += cv[j] * xv.y;
+        got[2] += cv[j] * xv.z;
+        got[3] += cv[j] * xv.w;
+      }
+    }
+    for (int kc = lane; kc < kchunks; kc += 64) {
+      const bf16x8 a = *reinterpret_cast<const bf16x8*>(A + (size_t)m * K + kc * 8);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float aj = (float)a[j];
+        const float* yk = y + (kc * 8 + j) * FV;
+#pragma unroll
+        for (int v = 0; v < FV; ++v) want[v] += aj * yk[v];
+      }
+    }
+#pragma unroll
+    for (int v = 0; v < FV; ++v) {
+      float g = got[v], w = want[v];
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) {
+        g += __shfl_xor(g, off, 64);
+        w += __shfl_xor(w, off, 64);
+      }
+      const float d = g - w;
+      d2 += d * d;
+      w2 += w * w;
+    }
+  }
+  // every lane holds the wave's totals after the butterfly: lane 0 publishes them
+  if (lane == 0) {
+    red[0][wave] = d2;
+    red[1][wave] = w2;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    float a = 0.f, b = 0.f;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) {
+      a += red[0][w];
+      b += red[1][w];
+    }
+    out2[0] = a;
+    out2[1] = b;
+  }
+}
+
 }  // namespace amdprobe

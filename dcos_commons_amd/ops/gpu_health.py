@@ -38,24 +38,14 @@ def freivalds_rel_err(a, bt, c, generator, vectors: int = 4) -> float:
 
 
 def readiness_probe(device: int = 0) -> dict:
-    """The fast form used as a pod readiness check: numerics + memory integrity only."""
-    import torch
-
+    """The fast form used as a pod readiness check: numerics + memory integrity only, as ONE
+    native call (``ops.readiness``): hashed bf16 operands, the MFMA GEMM, Freivalds' check and the
+    64 MiB pattern test on a private stream with a single read-back. It sits on the deploy and
+    recovery critical path of every GPU pod, and the GIL is released while it runs."""
     from dcos_commons_amd import ops
 
     t0 = time.perf_counter()
-    dev = torch.device("cuda", device)
-    # the HIP kernels launch on the current device's stream: make `device` current for the probe
-    with torch.cuda.device(dev):
-        g = torch.Generator(device=dev)
-        g.manual_seed(4321 + device)
-        a = torch.randn((256, 512), generator=g, device=dev, dtype=torch.float32).to(torch.bfloat16)
-        bt = torch.randn((256, 512), generator=g, device=dev, dtype=torch.float32).to(torch.bfloat16)
-        c = ops.gemm_bf16_nt(a, bt)
-        rel = freivalds_rel_err(a, bt, c, g)
-        buf = torch.empty(16 * 2**20, dtype=torch.int32, device=dev)  # 64 MiB
-        ops.pattern_write(buf, seed=device + 11)
-        bad = ops.pattern_check(buf, seed=device + 11)
+    rel, bad = ops.readiness(device, seed=4321 + device)
     return {"device": device, "gemm_rel_err": rel, "mem_bad_words": bad,
             "healthy": bool(rel < MAX_GEMM_REL_ERR and bad == 0), "probe_seconds": round(time.perf_counter() - t0, 4)}
 

@@ -9,6 +9,7 @@ reconciliation TASK_UNKNOWN is handled as TASK_LOST (``SDK_UNKNOWN_AS_LOST``).
 from __future__ import annotations
 
 import logging
+import threading
 from typing import List, Optional
 
 from dcos_commons_amd.framework.process_exit import ProcessExit
@@ -43,6 +44,9 @@ class AbstractScheduler(MesosEventClient):
         self.launch_watchdog = LaunchWatchdog(_cfg(scheduler_config, "launch_reconcile_s", 0.0), namespace)
         self.unknown_as_lost = _cfg(scheduler_config, "is_unknown_as_lost", False)
         self.logger = logging.getLogger(type(self).__module__ + (f"({namespace})" if namespace else ""))
+        # set after every processed status: observers (benchmarks, tests) wait on it instead of
+        # polling plan state
+        self.status_processed = threading.Event()
 
     def customize_plans(self) -> None:
         if self.plan_customizer is None:
@@ -125,6 +129,8 @@ class AbstractScheduler(MesosEventClient):
             self.logger.warning("Failed to update TaskStatus received from Mesos: %s", e)
         except Exception as e:  # noqa: BLE001
             self.logger.warning("Failed to update TaskStatus received from Mesos: %s", e)
+        finally:
+            self.status_processed.set()
         return TaskStatusResponse.processed()
 
     # abstract

@@ -482,3 +482,62 @@ def test_held_offers_survive_concurrent_rescinds(drv):
         stop.set()
         t.join()
     assert errors == []
+
+
+# ---------------------------------------------------------------------------------------
+# MI355X offer-loop latency knobs: status wake-ups and revives that cannot bring new work
+
+
+def _st(state, check_exit=None, check=False):
+    s = P.TaskStatus(state=state)
+    s.task_id.value = "svc__task__1"
+    if check or check_exit is not None:
+        cs = s.check_status
+        cs.type = P.CheckInfo.COMMAND if hasattr(P, "CheckInfo") else 1
+        cs.command.SetInParent()
+        if check_exit is not None:
+            cs.command.exit_code = check_exit
+    return s
+
+
+@pytest.mark.parametrize("status,wakes", [
+    (_st(P.TASK_STAGING), False),
+    (_st(P.TASK_STARTING), False),
+    (_st(P.TASK_RUNNING, check=True), False),          # readiness check still pending
+    (_st(P.TASK_RUNNING, check_exit=0), True),         # readiness passed: the step completes
+    (_st(P.TASK_RUNNING, check_exit=1), True),         # readiness failed
+    (_st(P.TASK_RUNNING), True),                       # no readiness check: RUNNING completes
+    (_st(P.TASK_FAILED), True),
+    (_st(P.TASK_LOST), True),
+    (_st(P.TASK_FINISHED), True),
+    (_st(P.TASK_KILLED), True),
+])
+def test_only_statuses_that_can_create_work_wake_the_offer_loop(status, wakes):
+    from dcos_commons_amd.framework.framework_scheduler import can_create_work
+
+    assert can_create_work(status) is wakes
+
+
+class _Step:
+    def __init__(self, pending):
+        self.pending = pending
+
+    def is_pending(self):
+        return self.pending
+
+    def is_prepared(self):
+        return False
+
+
+@pytest.mark.parametrize("flag,pending,revives", [
+    (True, False, 0),    # the new work launched from offers in hand: no revive
+    (True, True, 1),     # a candidate is still unmatched: revive for more offers
+    (False, False, 1),   # reference: every new work set revives
+])
+def test_revive_only_for_unmatched_new_work(drv, flag, pending, revives):
+    client = Client(status=ClientStatusResponse.launching(True))
+    client.candidate_steps = [_Step(pending)]
+    p = processor(client, revive_only_unmatched=flag).disable_threading()
+    p.start()
+    p.enqueue([offer("a")])
+    assert drv.revives == revives

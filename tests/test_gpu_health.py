@@ -19,61 +19,24 @@ def test_freivalds_check_matches_dense_reference():
     assert 0.3 < projected / dense < 3
 
 
-def test_readiness_probe_runs_its_kernels_on_the_requested_device(monkeypatch):
-    """the readiness probe makes its device current for the HIP launches and restores
-    the caller's device afterwards (gpu_health.py ``torch.cuda.device(dev)``). The one-GPU box
-    cannot show this (``test_readiness_probe_on_a_non_default_device`` skips there), so the device
-    bookkeeping is checked here with the CUDA runtime replaced by a recorder. The multi-GPU
-    hardware path itself stays unverified until a multi-GPU run exists."""
-    import contextlib
-
-    import torch
-
+def test_readiness_probe_is_one_native_call_on_the_requested_device(monkeypatch):
+    """The readiness probe hands the whole check of ``device`` to ``ops.readiness`` (one native
+    call that makes the device current for its launches and restores the caller's device,
+    csrc/probe_api.hip ``DeviceGuard``) and judges the two numbers it returns. The device
+    bookkeeping itself runs on the GPU box (test_gpu_ops); this pins the Python contract."""
     from dcos_commons_amd import ops
     from dcos_commons_amd.ops import gpu_health
 
-    current = {"dev": 0}
-    seen = []
+    calls = []
+    answers = iter([(2e-7, 0), (5e-3, 0), (2e-7, 3)])
 
-    @contextlib.contextmanager
-    def fake_device(dev):
-        idx = dev.index if isinstance(dev, torch.device) else int(dev)
-        prev, current["dev"] = current["dev"], idx
-        try:
-            yield
-        finally:
-            current["dev"] = prev
+    def fake_readiness(device, seed=0, inject=0):
+        calls.append((device, seed, inject))
+        return next(answers)
 
-    real_gen, real_randn, real_empty = torch.Generator, torch.randn, torch.empty
-
-    def on_cpu(fn):
-        def wrapped(*a, **kw):
-            kw.pop("device", None)
-            return fn(*a, **kw)
-        return wrapped
-
-    def gemm(a, bt):
-        seen.append(("gemm", current["dev"]))
-        return a.float() @ bt.float().t()
-
-    def pattern_write(buf, seed):
-        seen.append(("write", current["dev"]))
-
-    def pattern_check(buf, seed):
-        seen.append(("check", current["dev"]))
-        return 0
-
-    monkeypatch.setattr(torch.cuda, "device", fake_device)
-    monkeypatch.setattr(torch.cuda, "current_device", lambda: current["dev"])
-    monkeypatch.setattr(torch, "Generator", on_cpu(real_gen))
-    monkeypatch.setattr(torch, "randn", on_cpu(real_randn))
-    monkeypatch.setattr(torch, "empty", lambda *a, **kw: real_empty(8, dtype=kw.get("dtype")))
-    monkeypatch.setattr(ops, "gemm_bf16_nt", gemm)
-    monkeypatch.setattr(ops, "pattern_write", pattern_write)
-    monkeypatch.setattr(ops, "pattern_check", pattern_check)
-
-    current["dev"] = 2  # the caller's device
-    rep = gpu_health.readiness_probe(device=5)
-    assert rep["healthy"] and rep["device"] == 5
-    assert seen == [("gemm", 5), ("write", 5), ("check", 5)]
-    assert torch.cuda.current_device() == 2  # restored
+    monkeypatch.setattr(ops, "readiness", fake_readiness)
+    healthy = gpu_health.readiness_probe(device=5)
+    assert healthy["healthy"] and healthy["device"] == 5 and healthy["mem_bad_words"] == 0
+    assert not gpu_health.readiness_probe(device=5)["healthy"]     # GEMM error above 1e-3
+    assert not gpu_health.readiness_probe(device=5)["healthy"]     # bad memory words
+    assert calls == [(5, 4326, 0)] * 3

@@ -138,3 +138,104 @@ def test_readiness_probe_on_a_non_default_device(dev):
     rep = readiness_probe(1)
     assert rep["healthy"], rep
     assert torch.cuda.current_device() == 0       # the caller's current device is restored
+
+
+# ---------------------------------------------------------------------------------------
+# fused readiness path (csrc/probe_kernels.hip readiness_prep_kernel / freivalds_kernel,
+# csrc/probe_api.hip amdprobe_readiness)
+
+
+@pytest.mark.parametrize("m,n,k", [(256, 256, 512), (128, 384, 64), (512, 128, 1024), (64, 20, 40)])
+def test_freivalds_kernel_matches_fp32_reference(dev, m, n, k):
+    from dcos_commons_amd import ops
+
+    g = torch.Generator(device=dev)
+    g.manual_seed(m + 3 * n + 7 * k)
+    a = torch.randn((m, k), generator=g, device=dev).to(torch.bfloat16)
+    bt = torch.randn((n, k), generator=g, device=dev).to(torch.bfloat16)
+    x = torch.randn((n, 4), generator=g, device=dev)
+    c = a.float() @ bt.float().t()
+    want = a.float() @ (bt.float().t() @ x)
+    d2, w2 = ops.freivalds(a, bt, c, x)
+    ref_w2 = float((want * want).sum())
+    assert abs(w2 - ref_w2) / ref_w2 < 1e-4
+    assert (d2 / w2) ** 0.5 < 1e-5                     # an exact product passes
+    bad = c.clone()
+    bad[:16, :16] = 0                                  # one lost MFMA tile
+    got = bad @ x
+    ref_d2 = float(((got - want) ** 2).sum())
+    d2b, w2b = ops.freivalds(a, bt, bad, x)
+    assert abs(d2b - ref_d2) / ref_d2 < 1e-3
+    if m >= 16 and n >= 16:
+        d2i, _ = ops.freivalds(a, bt, c, x, inject=1)  # the planted fault: the same tile read as zeros
+        assert abs(d2i - ref_d2) / ref_d2 < 1e-3
+
+
+def _mix32(v):
+    import numpy as np
+
+    v = v ^ (v >> np.uint64(33))
+    v = v * np.uint64(0xFF51AFD7ED558CCD)
+    v = v ^ (v >> np.uint64(33))
+    v = v * np.uint64(0xC4CEB9FE1A85EC53)
+    v = v ^ (v >> np.uint64(33))
+    return (v & np.uint64(0xFFFFFFFF)).astype(np.uint32)
+
+
+def test_readiness_fill_matches_the_host_hash(dev):
+    import numpy as np
+
+    from dcos_commons_amd import ops
+
+    seed = 4321
+    ab = torch.empty(4096, dtype=torch.int32, device=dev)      # 1024 chunks of 16 B
+    x = torch.empty(1024, dtype=torch.float32, device=dev)
+    ops.readiness_fill(ab, x, seed)
+    torch.cuda.synchronize()
+    with np.errstate(over="ignore"):
+        i = np.arange(1024, dtype=np.uint64)
+        base = (i << np.uint64(2)) ^ (np.uint64(seed) << np.uint64(40))
+        words = np.stack([_mix32(base + np.uint64(j)) for j in range(4)], axis=1).reshape(-1)
+        words = (words & np.uint32(0x807F807F)) | np.uint32(0x3F003F00)
+        xb = (i << np.uint64(2)) ^ (np.uint64(seed ^ 0x9E3779B9) << np.uint64(40))
+        xs = (_mix32(xb) >> np.uint32(8)).astype(np.float32) * np.float32(2.0 / 16777216.0) - np.float32(1.0)
+    assert np.array_equal(ab.cpu().numpy().view(np.uint32), words)
+    assert np.array_equal(x.cpu().numpy(), xs)
+    vals = ab.view(torch.bfloat16).float().abs()
+    assert bool(((vals >= 0.5) & (vals < 1.0)).all())
+
+
+def test_fused_readiness_passes_and_catches_planted_faults(dev):
+    import time
+
+    from dcos_commons_amd import ops
+    from dcos_commons_amd.ops.gpu_health import MAX_GEMM_REL_ERR
+
+    rel, bad = ops.readiness(0, seed=4321)
+    assert rel < 1e-4 and bad == 0
+    again = ops.readiness(0, seed=4321)               # same data; LDS atomics reorder fp32 sums only
+    assert again[1] == 0 and again[0] == pytest.approx(rel, rel=0.2, abs=1e-9)
+    rel1, bad1 = ops.readiness(0, seed=4321, inject=1)
+    assert rel1 > MAX_GEMM_REL_ERR and bad1 == 0
+    rel2, bad2 = ops.readiness(0, seed=4321, inject=2)
+    assert rel2 < 1e-4 and bad2 >= 1
+    assert ops.readiness(0, seed=7)[1] == 0
+    with pytest.raises(ops.ProbeError):
+        ops.readiness(torch.cuda.device_count(), seed=1)
+    assert torch.cuda.current_device() == 0                     # the caller's device is kept
+    t0 = time.perf_counter()
+    for _ in range(20):
+        ops.readiness(0, seed=4321)
+    per_call_ms = (time.perf_counter() - t0) / 20 * 1e3
+    print(f"fused readiness: {per_call_ms:.3f} ms per call")
+    assert per_call_ms < 5.0
+
+
+def test_fused_readiness_from_many_threads(dev):
+    from concurrent.futures import ThreadPoolExecutor
+
+    from dcos_commons_amd import ops
+
+    with ThreadPoolExecutor(8) as pool:
+        results = list(pool.map(lambda s: ops.readiness(0, seed=s), range(32)))
+    assert all(rel < 1e-4 and bad == 0 for rel, bad in results)

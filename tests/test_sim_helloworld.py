@@ -24,7 +24,8 @@ def runner(**env):
     e = dict(ENV)
     e.update(env)
     # reference cadence: every work-set change revives immediately (no burst spacing in the sim)
-    return ServiceTestRunner(SVC).set_env(e).set_scheduler_env(SDK_REVIVE_INTERVAL_S="0", SDK_FAST_UNSUPPRESS="false")
+    return ServiceTestRunner(SVC).set_env(e).set_scheduler_env(SDK_REVIVE_INTERVAL_S="0", SDK_FAST_UNSUPPRESS="false",
+                                                               SDK_REVIVE_ONLY_UNMATCHED="false")
 
 
 def default_deployment_ticks():
