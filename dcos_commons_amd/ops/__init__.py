@@ -50,9 +50,9 @@ def _bind(lib: ctypes.CDLL) -> None:
     lib.amdprobe_pattern_write.restype = i
     lib.amdprobe_pattern_check.argtypes = [vp, sz, ctypes.c_uint, vp, i, vp]
     lib.amdprobe_pattern_check.restype = i
-    lib.amdprobe_freivalds.argtypes = [vp, vp, vp, vp, i, i, i, i, vp, vp]
-    lib.amdprobe_freivalds.restype = i
-    lib.amdprobe_readiness_fill.argtypes = [vp, sz, vp, i, ctypes.c_uint, vp, vp]
+    lib.amdprobe_gemm_check.argtypes = [vp, vp, vp, i, i, i, i, vp, vp]
+    lib.amdprobe_gemm_check.restype = i
+    lib.amdprobe_readiness_fill.argtypes = [vp, sz, ctypes.c_uint, vp, vp]
     lib.amdprobe_readiness_fill.restype = i
     lib.amdprobe_readiness.argtypes = [i, ctypes.c_uint, i, ctypes.POINTER(d), ctypes.POINTER(ctypes.c_ulonglong)]
     lib.amdprobe_readiness.restype = i
@@ -153,31 +153,31 @@ def pattern_check(buf, seed: int, blocks: int = 2048) -> int:
     return int(errs.item())
 
 
-def freivalds(a, bt, c, x, inject: int = 0):
-    """Freivalds' check of ``c == a @ bt.T`` with the columns of ``x`` (``N x 4`` fp32): returns
-    ``(||c x - a (bt^T x)||^2, ||a (bt^T x)||^2)`` computed on the GPU (one workgroup)."""
+def gemm_check(a, bt, c, inject: int = 0):
+    """Dense check of ``c == a @ bt.T`` on the GPU (an fp32 VALU reference per element): returns
+    ``(sum((c - a bt^T)^2), sum((a bt^T)^2))``. M, N % 16 == 0, K % 8 == 0, K <= 1024."""
     import torch
 
     m, k = a.shape
     n = bt.shape[0]
     if a.dtype != torch.bfloat16 or bt.dtype != torch.bfloat16 or c.dtype != torch.float32 or \
-            x.dtype != torch.float32 or tuple(c.shape) != (m, n) or tuple(x.shape) != (n, 4) or bt.shape[1] != k:
-        raise ProbeError(f"freivalds: bad operands {tuple(a.shape)} {tuple(bt.shape)} {tuple(c.shape)} {tuple(x.shape)}")
-    a, bt, c, x = a.contiguous(), bt.contiguous(), c.contiguous(), x.contiguous()
+            tuple(c.shape) != (m, n) or bt.shape[1] != k:
+        raise ProbeError(f"gemm_check: bad operands {tuple(a.shape)} {tuple(bt.shape)} {tuple(c.shape)}")
+    a, bt, c = a.contiguous(), bt.contiguous(), c.contiguous()
     out = torch.zeros(4, dtype=torch.float32, device=a.device)
-    _check(lib().amdprobe_freivalds(a.data_ptr(), bt.data_ptr(), c.data_ptr(), x.data_ptr(), m, n, k, inject,
-                                    out.data_ptr(), _stream(a.device)), "freivalds")
+    _check(lib().amdprobe_gemm_check(a.data_ptr(), bt.data_ptr(), c.data_ptr(), m, n, k, inject, out.data_ptr(),
+                                     _stream(a.device)), "gemm_check")
     o = out.cpu()
     return float(o[0]), float(o[1])
 
 
-def readiness_fill(ab, x, seed: int):
-    """The readiness operand fill into ``ab`` (any dtype, byte size % 16) and ``x`` (fp32)."""
+def readiness_fill(ab, seed: int):
+    """The readiness operand fill into ``ab`` (any dtype, byte size % 16)."""
     import torch
 
     res = torch.empty(8, dtype=torch.int32, device=ab.device)
-    _check(lib().amdprobe_readiness_fill(ab.data_ptr(), ab.numel() * ab.element_size(), x.data_ptr(), x.numel(),
-                                         seed & 0xFFFFFFFF, res.data_ptr(), _stream(ab.device)), "readiness_fill")
+    _check(lib().amdprobe_readiness_fill(ab.data_ptr(), ab.numel() * ab.element_size(), seed & 0xFFFFFFFF,
+                                         res.data_ptr(), _stream(ab.device)), "readiness_fill")
 
 
 READINESS_SHAPE = (256, 256, 512)   # M, N, K of the readiness GEMM (csrc/probe_api.hip)
@@ -186,8 +186,8 @@ READINESS_PATTERN_BYTES = 64 << 20
 
 def readiness(device: int = 0, seed: int = 0, inject: int = 0):
     """The whole readiness check of one device in one native call (no framework ops): hashed bf16
-    operands, the MFMA GEMM, Freivalds' check and the 64 MiB HBM pattern test on a private
-    stream, then one 32-byte read-back. Returns ``(gemm_rel_err, bad_words)``. ``inject`` = 1 or
+    operands, the MFMA GEMM, a dense fp32 check of every product element and the 64 MiB HBM
+    pattern test on a private stream, then one 32-byte read-back. Returns ``(gemm_rel_err, bad_words)``. ``inject`` = 1 or
     2 plants a product / memory fault (tests). The GIL is released for the duration (ctypes)."""
     rel = ctypes.c_double(0.0)
     bad = ctypes.c_ulonglong(0)

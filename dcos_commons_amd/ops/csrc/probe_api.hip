@@ -81,25 +81,24 @@ AMDPROBE_EXPORT int amdprobe_pattern_check(const void* p, size_t bytes, unsigned
   return (int)hipGetLastError();
 }
 
-// Freivalds' check of C = A Bt^T against FV = 4 vectors X (N x 4 fp32): writes
-// out2[0] = ||C X - A (Bt^T X)||^2, out2[1] = ||A (Bt^T X)||^2 (device pointer, 2 floats).
-AMDPROBE_EXPORT int amdprobe_freivalds(const void* A, const void* Bt, const float* C, const float* X, int M, int N,
-                                       int K, int inject, float* out2, void* stream) {
-  if (M <= 0 || N <= 0 || K <= 0 || N % 4 || K % 8 || K > FREIVALDS_MAX_K) return ERR_SHAPE;
-  if (!aligned16(A) || !aligned16(Bt) || !aligned16(C) || !aligned16(X)) return ERR_ALIGN;
-  hipLaunchKernelGGL(freivalds_kernel, dim3(1), dim3(FREIVALDS_THREADS), 0, (hipStream_t)stream, (const __bf16*)A,
-                     (const __bf16*)Bt, C, X, M, N, K, inject, out2);
+// Dense fp32 check of C = A Bt^T: adds sum((C - A Bt^T)^2) to out2[0] and sum((A Bt^T)^2) to
+// out2[1] (device pointer, 2 floats that the caller zeroes).
+AMDPROBE_EXPORT int amdprobe_gemm_check(const void* A, const void* Bt, const float* C, int M, int N, int K,
+                                        int inject, float* out2, void* stream) {
+  if (M <= 0 || N <= 0 || K <= 0 || M % CHECK_TILE || N % CHECK_TILE || K % 8 || K > CHECK_MAX_K) return ERR_SHAPE;
+  if (!aligned16(A) || !aligned16(Bt)) return ERR_ALIGN;
+  hipLaunchKernelGGL(gemm_check_kernel, dim3((M / CHECK_TILE) * (N / CHECK_TILE)), dim3(CHECK_THREADS), 0,
+                     (hipStream_t)stream, (const __bf16*)A, (const __bf16*)Bt, C, M, N, K, inject, out2);
   return (int)hipGetLastError();
 }
 
 // The readiness operand fill on its own (tests compare it with a host model of the hash):
-// `ab` gets `ab_bytes` of hashed bf16, `x` gets `nx` hashed floats in [-1, 1), `res` is zeroed.
-AMDPROBE_EXPORT int amdprobe_readiness_fill(void* ab, size_t ab_bytes, float* x, int nx, unsigned seed, void* res,
-                                            void* stream) {
-  if (ab_bytes == 0 || ab_bytes % 16 || nx < 0) return ERR_SHAPE;
-  if (!aligned16(ab) || !aligned16(x) || !aligned16(res)) return ERR_ALIGN;
+// `ab` gets `ab_bytes` of hashed bf16 and `res` (32 bytes) is zeroed.
+AMDPROBE_EXPORT int amdprobe_readiness_fill(void* ab, size_t ab_bytes, unsigned seed, void* res, void* stream) {
+  if (ab_bytes == 0 || ab_bytes % 16) return ERR_SHAPE;
+  if (!aligned16(ab) || !aligned16(res)) return ERR_ALIGN;
   hipLaunchKernelGGL(readiness_prep_kernel, dim3(64), dim3(256), 0, (hipStream_t)stream, (uint4*)ab, ab_bytes / 16,
-                     x, nx, (uint32_t)seed, (ReadinessResult*)res);
+                     (uint32_t)seed, (ReadinessResult*)res);
   return (int)hipGetLastError();
 }
 
@@ -107,7 +106,7 @@ AMDPROBE_EXPORT int amdprobe_readiness_fill(void* ab, size_t ab_bytes, float* x,
 // amdprobe_readiness: the whole readiness check of one device in one call (see the kernel file).
 // Buffers, a non-blocking stream and a pinned result slot are created on first use per device
 // and reused; calls for one device serialize on its context. The calling thread's current device
-// is restored. inject: 0 = none, 1 = lose one 16x16 tile of the product (Freivalds must fail), 2 = corrupt one
+// is restored. inject: 0 = none, 1 = lose one 16x16 tile of the product (the check must fail), 2 = corrupt one
 // pattern word (the memory check must count it). Returns 0 or a HIP error / negative shape code.
 // ---------------------------------------------------------------------------------------
 namespace {
@@ -121,7 +120,6 @@ struct ReadinessCtx {
   hipStream_t stream = nullptr;
   __bf16* ab = nullptr;          // A (RM x RK) then Bt (RN x RK)
   float* c = nullptr;            // RM x RN
-  float* x = nullptr;            // RN x FV
   uint4* pattern = nullptr;
   ReadinessResult* res = nullptr;
   ReadinessResult* host = nullptr;  // pinned
@@ -149,7 +147,6 @@ int readiness_init(ReadinessCtx& ctx) {
   PROBE_TRY(hipStreamCreateWithFlags(&ctx.stream, hipStreamNonBlocking));
   PROBE_TRY(hipMalloc((void**)&ctx.ab, size_t(RM + RN) * RK * sizeof(__bf16)));
   PROBE_TRY(hipMalloc((void**)&ctx.c, size_t(RM) * RN * sizeof(float)));
-  PROBE_TRY(hipMalloc((void**)&ctx.x, size_t(RN) * FV * sizeof(float)));
   PROBE_TRY(hipMalloc((void**)&ctx.pattern, PATTERN_BYTES));
   PROBE_TRY(hipMalloc((void**)&ctx.res, sizeof(ReadinessResult)));
   PROBE_TRY(hipHostMalloc((void**)&ctx.host, sizeof(ReadinessResult), hipHostMallocDefault));
@@ -175,12 +172,13 @@ AMDPROBE_EXPORT int amdprobe_readiness(int device, unsigned seed, int inject, do
   const __bf16* A = ctx.ab;
   const __bf16* Bt = ctx.ab + size_t(RM) * RK;
   hipLaunchKernelGGL(readiness_prep_kernel, dim3(64), dim3(256), 0, s, (uint4*)ctx.ab,
-                     size_t(RM + RN) * RK * sizeof(__bf16) / 16, ctx.x, RN * FV, (uint32_t)seed, ctx.res);
+                     size_t(RM + RN) * RK * sizeof(__bf16) / 16, (uint32_t)seed, ctx.res);
   PROBE_TRY(hipGetLastError());
-  const int rc = amdprobe_gemm_bf16_nt(A, Bt, ctx.c, RM, RN, RK, s);
+  // 128x128 tiles: four workgroups for the 256x256 product (one 256x256-tile workgroup takes ~15 us)
+  const int rc = amdprobe_gemm_bf16_nt_variant(A, Bt, ctx.c, RM, RN, RK, 1, s);
   if (rc) return rc;
-  hipLaunchKernelGGL(freivalds_kernel, dim3(1), dim3(FREIVALDS_THREADS), 0, s, A, Bt, (const float*)ctx.c,
-                     (const float*)ctx.x, RM, RN, RK, inject == 1 ? 1 : 0, &ctx.res->diff2);
+  hipLaunchKernelGGL(gemm_check_kernel, dim3((RM / CHECK_TILE) * (RN / CHECK_TILE)), dim3(CHECK_THREADS), 0, s, A,
+                     Bt, (const float*)ctx.c, RM, RN, RK, inject == 1 ? 1 : 0, &ctx.res->diff2);
   PROBE_TRY(hipGetLastError());
   hipLaunchKernelGGL(pattern_write_kernel, dim3(2048), dim3(256), 0, s, ctx.pattern, PATTERN_BYTES / 16,
                      (uint32_t)seed);
@@ -191,7 +189,7 @@ AMDPROBE_EXPORT int amdprobe_readiness(int device, unsigned seed, int inject, do
   PROBE_TRY(hipGetLastError());
   PROBE_TRY(hipMemcpyAsync(ctx.host, ctx.res, sizeof(ReadinessResult), hipMemcpyDeviceToHost, s));
   PROBE_TRY(hipStreamSynchronize(s));
-  const double d2 = ctx.host->diff2, w2 = ctx.host->want2;
+  const double d2 = ctx.host->diff2, w2 = ctx.host->ref2;
   *rel_err = w2 > 0.0 ? std::sqrt(d2 / w2) : HUGE_VAL;
   *bad_words = ctx.host->bad_words;
   return 0;

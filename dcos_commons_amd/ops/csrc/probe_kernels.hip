@@ -458,31 +458,20 @@ void pattern_check_kernel(const uint4* __restrict__ p, size_t n16, uint32_t seed
 // Fused readiness check. A pod's readiness probe is on the deploy / recovery critical path, so
 // it runs as ONE host call: five launches back to back on a private stream and a single 32-byte
 // read-back, instead of a chain of framework ops with a host sync in the middle.
-//   readiness_prep_kernel  A, Bt <- hashed bf16 operands, X <- hashed fp32 vectors, result <- 0
+//   readiness_prep_kernel  A, Bt <- hashed bf16 operands, result <- 0
 //   gemm (MFMA)            C = A Bt^T
-//   freivalds_kernel       ||C X - A (Bt^T X)||^2 and ||A (Bt^T X)||^2 (Freivalds' check:
-//                          O(MN + NK + MK) work instead of a second GEMM)
+//   gemm_check_kernel      every element of C against an fp32 VALU reference (v_dot2_f32_bf16)
 //   pattern_write/check    address-hashed write + verify over a 64 MiB buffer
 // ---------------------------------------------------------------------------------------
 struct ReadinessResult {
-  float diff2;                  // sum over (m, v) of (C X - A (Bt^T X))^2
-  float want2;                  // sum over (m, v) of (A (Bt^T X))^2
+  float diff2;                  // sum over (m, n) of (C - A Bt^T)^2, reference in fp32
+  float ref2;                   // sum over (m, n) of (A Bt^T)^2
   unsigned long long bad_words;
   unsigned long long reserved;
 };
 
-constexpr int FV = 4;           // Freivalds vectors
-constexpr int FREIVALDS_THREADS = 1024;
-constexpr int FREIVALDS_MAX_K = 4096;
-
-__device__ __forceinline__ float hashed_unit(uint64_t i, uint32_t seed) {
-  // uniform in [-1, 1) from the top 24 bits of the hash
-  return (float)(mix32((i << 2) ^ ((uint64_t)(seed ^ 0x9E3779B9u) << 40)) >> 8) * (2.0f / 16777216.0f) - 1.0f;
-}
-
 __global__ __launch_bounds__(256)
-void readiness_prep_kernel(uint4* __restrict__ ab, size_t ab16, float* __restrict__ x, int nx, uint32_t seed,
-                           ReadinessResult* __restrict__ res) {
+void readiness_prep_kernel(uint4* __restrict__ ab, size_t ab16, uint32_t seed, ReadinessResult* __restrict__ res) {
   const size_t tid = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
   const size_t stride = (size_t)gridDim.x * blockDim.x;
   for (size_t i = tid; i < ab16; i += stride) {
@@ -495,99 +484,69 @@ void readiness_prep_kernel(uint4* __restrict__ ab, size_t ab16, float* __restric
     v.w = (v.w & 0x807F807Fu) | 0x3F003F00u;
     ab[i] = v;
   }
-  for (size_t i = tid; i < (size_t)nx; i += stride) x[i] = hashed_unit(i, seed);
   if (tid == 0) {
     res->diff2 = 0.f;
-    res->want2 = 0.f;
+    res->ref2 = 0.f;
     res->bad_words = 0ull;
     res->reserved = 0ull;
   }
 }
 
-// One workgroup of 16 waves. X is N x FV (row-major), C is M x N fp32, A is M x K and Bt is N x K
-// bf16 (K-contiguous). Requires N % 4 == 0, K % 8 == 0, K <= FREIVALDS_MAX_K (host-checked).
-// `inject` = 1 reads C[0:16][0:16] as zeros, a lost MFMA tile (tests that the check catches it).
-__global__ __launch_bounds__(FREIVALDS_THREADS)
-void freivalds_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, const float* __restrict__ C,
-                      const float* __restrict__ X, int M, int N, int K, int inject, float* __restrict__ out2) {
-  __shared__ float y[FREIVALDS_MAX_K * FV];   // y = Bt^T X   (K x FV)
-  __shared__ float red[2][FREIVALDS_THREADS / 64];
+// Dense check of C = A Bt^T: one workgroup per 16 x 16 output tile (M / 16 * N / 16 of them, so
+// a 256 x 256 product spreads over 256 CUs). The tile's 16 A rows and 16 Bt rows are staged in
+// LDS (rows padded by 16 B: the 16 Bt rows a wave reads at one k land on disjoint bank groups),
+// each thread forms its element's fp32 reference with v_dot2_f32_bf16 (two accumulators), and
+// the workgroup adds its sum of squared differences and of squared references to out2 with two
+// float atomics (out2 must arrive zeroed; the prep kernel zeroes it). Needs M, N % 16 == 0,
+// K % 8 == 0, K <= CHECK_MAX_K (host-checked). `inject` = 1 reads C[0:16][0:16] as zeros, a
+// lost MFMA tile (tests that the check catches it).
+constexpr int CHECK_TILE = 16;
+constexpr int CHECK_THREADS = CHECK_TILE * CHECK_TILE;
+constexpr int CHECK_MAX_K = 1024;
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+
+__global__ __launch_bounds__(CHECK_THREADS)
+void gemm_check_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ Bt, const float* __restrict__ C,
+                       int M, int N, int K, int inject, float* __restrict__ out2) {
+  __shared__ __attribute__((aligned(16))) __bf16 la[CHECK_TILE * (CHECK_MAX_K + 8)];
+  __shared__ __attribute__((aligned(16))) __bf16 lb[CHECK_TILE * (CHECK_MAX_K + 8)];
+  __shared__ float red[2][CHECK_THREADS / 64];
+  const int tiles_n = N / CHECK_TILE;
+  const int tm = blockIdx.x / tiles_n, tn = blockIdx.x - tm * tiles_n;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  constexpr int NW = FREIVALDS_THREADS / 64;
-  for (int i = tid; i < K * FV; i += FREIVALDS_THREADS) y[i] = 0.f;
-  __syncthreads();
-
-  // phase 1: wave w sums rows n = w, w + 16, ... of Bt; each lane owns 8 consecutive k per chunk
-  // (one 16-B load per row), partial sums merged with LDS atomics
+  const int row = K + 8;                       // LDS row stride (bf16)
   const int kchunks = K / 8;
-  for (int kc = lane; kc < kchunks; kc += 64) {
-    float s[8][FV];
-#pragma unroll
-    for (int j = 0; j < 8; ++j)
-#pragma unroll
-      for (int v = 0; v < FV; ++v) s[j][v] = 0.f;
-#pragma unroll 4
-    for (int n = wave; n < N; n += NW) {
-      const bf16x8 b = *reinterpret_cast<const bf16x8*>(Bt + (size_t)n * K + kc * 8);
-      const float4 xv = *reinterpret_cast<const float4*>(X + (size_t)n * FV);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float bj = (float)b[j];
-        s[j][0] += bj * xv.x;
-        s[j][1] += bj * xv.y;
-        s[j][2] += bj * xv.z;
-        s[j][3] += bj * xv.w;
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < 8; ++j)
-#pragma unroll
-      for (int v = 0; v < FV; ++v) atomicAdd(&y[(kc * 8 + j) * FV + v], s[j][v]);
+  for (int i = tid; i < CHECK_TILE * kchunks; i += CHECK_THREADS) {
+    const int r = i / kchunks, kc = i - r * kchunks;
+    *reinterpret_cast<uint4*>(la + r * row + kc * 8) =
+        *reinterpret_cast<const uint4*>(A + (size_t)(tm * CHECK_TILE + r) * K + kc * 8);
+    *reinterpret_cast<uint4*>(lb + r * row + kc * 8) =
+        *reinterpret_cast<const uint4*>(Bt + (size_t)(tn * CHECK_TILE + r) * K + kc * 8);
   }
   __syncthreads();
-
-  // phase 2: one wave per row m: got = C[m, :] X, want = A[m, :] y, reduced across the wave
-  float d2 = 0.f, w2 = 0.f;
-  const int nchunks = N / 4;
-  for (int m = wave; m < M; m += NW) {
-    float got[FV] = {0.f, 0.f, 0.f, 0.f}, want[FV] = {0.f, 0.f, 0.f, 0.f};
-    for (int nc = lane; nc < nchunks; nc += 64) {
-      float4 c = *reinterpret_cast<const float4*>(C + (size_t)m * N + nc * 4);
-      if (inject == 1 && m < 16 && nc < 4) c = make_float4(0.f, 0.f, 0.f, 0.f);   // a lost 16x16 tile
-      const float cv[4] = {c.x, c.y, c.z, c.w};
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const float4 xv = *reinterpret_cast<const float4*>(X + (size_t)(nc * 4 + j) * FV);
-        got[0] += cv[j] * xv.x;
-        got[1] += cv[j] * xv.y;
-        got[2] += cv[j] * xv.z;
-        got[3] += cv[j] * xv.w;
-      }
-    }
-    for (int kc = lane; kc < kchunks; kc += 64) {
-      const bf16x8 a = *reinterpret_cast<const bf16x8*>(A + (size_t)m * K + kc * 8);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float aj = (float)a[j];
-        const float* yk = y + (kc * 8 + j) * FV;
-#pragma unroll
-        for (int v = 0; v < FV; ++v) want[v] += aj * yk[v];
-      }
-    }
-#pragma unroll
-    for (int v = 0; v < FV; ++v) {
-      float g = got[v], w = want[v];
-#pragma unroll
-      for (int off = 32; off > 0; off >>= 1) {
-        g += __shfl_xor(g, off, 64);
-        w += __shfl_xor(w, off, 64);
-      }
-      const float d = g - w;
-      d2 += d * d;
-      w2 += w * w;
-    }
+  const int r = tid >> 4, c = tid & 15;
+  const __bf16* pa = la + r * row;
+  const __bf16* pb = lb + c * row;
+  float acc0 = 0.f, acc1 = 0.f;
+  for (int kc = 0; kc < kchunks; ++kc) {
+    const bf16x8 a8 = *reinterpret_cast<const bf16x8*>(pa + kc * 8);
+    const bf16x8 b8 = *reinterpret_cast<const bf16x8*>(pb + kc * 8);
+    acc0 = __builtin_amdgcn_fdot2_f32_bf16(bf16x2{a8[0], a8[1]}, bf16x2{b8[0], b8[1]}, acc0, false);
+    acc1 = __builtin_amdgcn_fdot2_f32_bf16(bf16x2{a8[2], a8[3]}, bf16x2{b8[2], b8[3]}, acc1, false);
+    acc0 = __builtin_amdgcn_fdot2_f32_bf16(bf16x2{a8[4], a8[5]}, bf16x2{b8[4], b8[5]}, acc0, false);
+    acc1 = __builtin_amdgcn_fdot2_f32_bf16(bf16x2{a8[6], a8[7]}, bf16x2{b8[6], b8[7]}, acc1, false);
   }
-  // every lane holds the wave's totals after the butterfly: lane 0 publishes them
+  const float ref = acc0 + acc1;
+  const int m = tm * CHECK_TILE + r, n = tn * CHECK_TILE + c;
+  float cv = C[(size_t)m * N + n];
+  if (inject == 1 && m < 16 && n < 16) cv = 0.f;   // a lost 16x16 tile
+  const float d = cv - ref;
+  float d2 = d * d, w2 = ref * ref;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    d2 += __shfl_xor(d2, off, 64);
+    w2 += __shfl_xor(w2, off, 64);
+  }
   if (lane == 0) {
     red[0][wave] = d2;
     red[1][wave] = w2;
@@ -596,12 +555,12 @@ void freivalds_kernel(const __bf16* __restrict__ A, const __bf16* __restrict__ B
   if (tid == 0) {
     float a = 0.f, b = 0.f;
 #pragma unroll
-    for (int w = 0; w < NW; ++w) {
+    for (int w = 0; w < CHECK_THREADS / 64; ++w) {
       a += red[0][w];
       b += red[1][w];
     }
-    out2[0] = a;
-    out2[1] = b;
+    atomicAdd(&out2[0], a);
+    atomicAdd(&out2[1], b);
   }
 }
 
