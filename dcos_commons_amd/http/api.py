@@ -8,6 +8,7 @@ simulation harness (``Router.dispatch``).
 """
 from __future__ import annotations
 
+import functools
 import json
 import re
 import urllib.parse
@@ -137,9 +138,16 @@ class Route:
     regex: "re.Pattern" = None
 
     def __post_init__(self):
-        pattern = re.sub(r"\{(\w+):path\}", r"(?P<\1>.+)", self.template.rstrip("/") or "/")
-        pattern = re.sub(r"\{(\w+)\}", r"(?P<\1>[^/]+)", pattern)
-        self.regex = re.compile("^" + pattern + "/?$")
+        self.regex = _route_regex(self.template)
+
+
+@functools.lru_cache(maxsize=1024)
+def _route_regex(template: str) -> "re.Pattern":
+    """``/v1/plans/{plan}`` -> compiled matcher (cached: every scheduler start builds the same
+    few hundred routes)."""
+    pattern = re.sub(r"\{(\w+):path\}", r"(?P<\1>.+)", template.rstrip("/") or "/")
+    pattern = re.sub(r"\{(\w+)\}", r"(?P<\1>[^/]+)", pattern)
+    return re.compile("^" + pattern + "/?$")
 
 
 class Router:

@@ -995,7 +995,12 @@ class ServiceSpec:
         return json.dumps(self.to_dict(), indent=2)
 
     def to_json_bytes(self) -> bytes:
-        return json.dumps(self.to_dict(), separators=(",", ":")).encode("utf-8")
+        # the spec is immutable: serialize once (the loopback check and the config store both ask)
+        data = self.__dict__.get("_json_bytes")
+        if data is None:
+            data = json.dumps(self.to_dict(), separators=(",", ":")).encode("utf-8")
+            self.__dict__["_json_bytes"] = data
+        return data
 
     get_bytes = to_json_bytes
 
@@ -1020,6 +1025,21 @@ class ServiceSpec:
         return ServiceSpec.from_dict(json.loads(data.decode("utf-8")))
 
 
+_PARSED_SPECS: Dict[bytes, "ServiceSpec"] = {}
+_PARSED_SPECS_MAX = 32
+
+
+def _parse_cached(data: bytes) -> "ServiceSpec":
+    """JSON -> ServiceSpec, memoized by the exact bytes (specs are immutable, parsing is pure)."""
+    spec = _PARSED_SPECS.get(data)
+    if spec is None:
+        spec = ServiceSpec.from_json_bytes(data)
+        if len(_PARSED_SPECS) >= _PARSED_SPECS_MAX:
+            _PARSED_SPECS.pop(next(iter(_PARSED_SPECS)))
+        _PARSED_SPECS[data] = spec
+    return spec
+
+
 class ServiceSpecFactory:
     """ConfigurationFactory<ServiceSpec>: parses persisted JSON configs."""
 
@@ -1031,7 +1051,7 @@ def loopback_check(spec: ServiceSpec) -> ServiceSpecFactory:
     """DefaultServiceSpec.getConfigurationFactory: round-trip the spec through JSON and fail
     if the result differs (DefaultServiceSpec.java getConfigurationFactory)."""
     factory = ServiceSpecFactory()
-    loop = factory.parse(spec.to_json_bytes())
+    loop = _parse_cached(spec.to_json_bytes())
     if loop != spec:
         raise SpecValidationError(
             "Equality test failed: Loopback result is not equal to original:\n- Original:\n"
