@@ -306,6 +306,16 @@ class LocalMaster:
             heapq.heappush(self._heap, (self.clock() + max(0.0, delay), next(self._seq), fn, args))
             self._cond.notify()
 
+    def _after(self, delay: float, fn, *args) -> None:
+        """A task's next lifecycle step: due now, it runs right here (an agent drives its own task
+        from STARTING to RUNNING to its first check without queueing behind every other task's
+        events, so the first readiness checks start while later tasks are still launching);
+        otherwise it is scheduled."""
+        if delay <= 0 and threading.current_thread() is self._thread:
+            fn(*args)
+        else:
+            self._schedule(delay, fn, *args)
+
     def _run(self) -> None:
         while True:
             with self._cond:
@@ -837,7 +847,7 @@ class LocalMaster:
         if task.epoch != epoch or task.status.state in TERMINAL:
             return
         self._update(task, P.TASK_STARTING)
-        self._schedule(timing.running_s, self._lifecycle_running, task, epoch, timing)
+        self._after(timing.running_s, self._lifecycle_running, task, epoch, timing)
 
     def _lifecycle_running(self, task: _Task, epoch: int, timing: TaskTiming) -> None:
         if task.epoch != epoch or task.status.state in TERMINAL:
@@ -856,7 +866,7 @@ class LocalMaster:
         if info.HasField("check"):
             delay = (info.check.delay_seconds if timing.honor_check_delays else 0.0) + timing.check_exec_s
             if self._check_runner(task) is not None:
-                self._schedule(delay, self._run_check, task, epoch)
+                self._after(delay, self._run_check, task, epoch)   # submits to the check pool
             else:
                 self._schedule(delay, self._lifecycle_ready, task, epoch)
         if timing.finish_after_s is not None and not self._executes:
