@@ -143,13 +143,39 @@ struct DeviceGuard {
     if (e_ != hipSuccess) return (int)e_;                \
   } while (0)
 
-int readiness_init(ReadinessCtx& ctx) {
+void readiness_release(ReadinessCtx& ctx) {
+  if (ctx.stream != nullptr) (void)hipStreamDestroy(ctx.stream);
+  if (ctx.ab != nullptr) (void)hipFree(ctx.ab);
+  if (ctx.c != nullptr) (void)hipFree(ctx.c);
+  if (ctx.pattern != nullptr) (void)hipFree(ctx.pattern);
+  if (ctx.res != nullptr) (void)hipFree(ctx.res);
+  if (ctx.host != nullptr) (void)hipHostFree(ctx.host);
+  ctx.stream = nullptr;
+  ctx.ab = nullptr;
+  ctx.c = nullptr;
+  ctx.pattern = nullptr;
+  ctx.res = nullptr;
+  ctx.host = nullptr;
+}
+
+int readiness_alloc(ReadinessCtx& ctx) {
   PROBE_TRY(hipStreamCreateWithFlags(&ctx.stream, hipStreamNonBlocking));
   PROBE_TRY(hipMalloc((void**)&ctx.ab, size_t(RM + RN) * RK * sizeof(__bf16)));
   PROBE_TRY(hipMalloc((void**)&ctx.c, size_t(RM) * RN * sizeof(float)));
   PROBE_TRY(hipMalloc((void**)&ctx.pattern, PATTERN_BYTES));
   PROBE_TRY(hipMalloc((void**)&ctx.res, sizeof(ReadinessResult)));
   PROBE_TRY(hipHostMalloc((void**)&ctx.host, sizeof(ReadinessResult), hipHostMallocDefault));
+  return 0;
+}
+
+// The context lives for the process (one probe per pod launch reuses it); a failed allocation
+// releases whatever it got, so the next call starts clean instead of leaking.
+int readiness_init(ReadinessCtx& ctx) {
+  const int rc = readiness_alloc(ctx);
+  if (rc) {
+    readiness_release(ctx);
+    return rc;
+  }
   ctx.ready = true;
   return 0;
 }
