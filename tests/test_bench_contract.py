@@ -65,3 +65,28 @@ def test_bench_two_ranks_over_gloo():
     assert len(recs) == 1, p.stdout            # only rank 0 prints
     _check(recs[0], 2, 1, 1)
     assert recs[0]["config"]["parallelism"] == "agents2-ranks2"
+
+
+def test_deploy_bench_waits_on_status_events():
+    """The timed waits re-check the plan when a status was processed (no 1 ms polling)."""
+    import threading
+    import time
+
+    from dcos_commons_amd.benchmarks.deploy_bench import DeployBench
+
+    b = DeployBench(1, timeout_s=5)
+    ev, state = threading.Event(), {"done": False, "checks": 0}
+
+    def pred():
+        state["checks"] += 1
+        return state["done"]
+
+    def finish():
+        time.sleep(0.05)
+        state["done"] = True
+        ev.set()
+
+    threading.Thread(target=finish).start()
+    waited = b._wait(pred, "test", ev)
+    assert state["done"] and 0.04 < waited < 1.0
+    assert state["checks"] < 30          # woken by the event / 5 ms ticks, not a 1 ms poll loop

@@ -541,3 +541,13 @@ def test_revive_only_for_unmatched_new_work(drv, flag, pending, revives):
     p.start()
     p.enqueue([offer("a")])
     assert drv.revives == revives
+
+
+def test_scheduler_process_switch_interval_flag():
+    import sys
+
+    from dcos_commons_amd.scheduler.scheduler_config import SchedulerConfig
+
+    assert SchedulerConfig.for_testing().gil_switch_interval_s() == 0.02
+    assert SchedulerConfig.for_testing(SDK_GIL_SWITCH_INTERVAL_MS=0).gil_switch_interval_s() == 0.0
+    assert sys.getswitchinterval() > 0

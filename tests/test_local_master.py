@@ -88,3 +88,22 @@ def test_mount_disks_added_to_a_running_agent():
         assert len(m.agents[aid].spec.mount_disks) == 2
     finally:
         m.shutdown()
+
+
+def test_zero_delay_lifecycle_steps_run_inline_on_the_dispatcher_only():
+    """``_after``: due now and on the dispatcher thread, a task's next lifecycle step runs in
+    place (STARTING -> RUNNING -> check submission without queueing behind other tasks);
+    anything else is scheduled on the dispatcher."""
+    m = LocalMaster(allocation_interval_s=60)
+    try:
+        order = []
+        m.call(lambda: (m._after(0, order.append, "inline"), order.append("after-call")))
+        assert order == ["inline", "after-call"]          # ran in place, before the caller continued
+        done = threading.Event()
+        m._after(0, lambda: (order.append("scheduled"), done.set()))   # from a foreign thread
+        assert done.wait(5) and order[-1] == "scheduled"
+        late = threading.Event()
+        m.call(lambda: m._after(0.05, late.set))            # a positive delay is always scheduled
+        assert not late.is_set() and late.wait(5)
+    finally:
+        m.shutdown()
