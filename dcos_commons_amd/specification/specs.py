@@ -96,7 +96,27 @@ def ranges_value(ranges: List[Tuple[int, int]]) -> P.Value:
     return val
 
 
+_SCALAR, _RANGES = P.Value.SCALAR, P.Value.RANGES
+
+
 def value_to_json(v: P.Value) -> dict:
+    """``P.to_json(v)`` for the value shapes specs hold, without the generic reflection walk
+    (this runs for every resource of every spec serialization): the same dict the protobuf JSON
+    mapping produces, with 64-bit range bounds as strings. Other shapes take the generic path."""
+    if v.HasField("type") and not (v.HasField("set") or v.HasField("text")):
+        t = v.type
+        if t == _SCALAR and v.HasField("scalar") and not v.HasField("ranges"):
+            return {"type": "SCALAR", "scalar": {"value": v.scalar.value} if v.scalar.HasField("value") else {}}
+        if t == _RANGES and v.HasField("ranges") and not v.HasField("scalar"):
+            rs = []
+            for r in v.ranges.range:
+                d = {}
+                if r.HasField("begin"):
+                    d["begin"] = str(r.begin)
+                if r.HasField("end"):
+                    d["end"] = str(r.end)
+                rs.append(d)
+            return {"type": "RANGES", "ranges": {"range": rs} if rs else {}}
     return P.to_json(v)
 
 

@@ -508,3 +508,20 @@ def test_health_check_json_matches_the_reference_layout():
     assert to_json_string(hc) == (
         '{\n  "command" : "some-command",\n  "max-consecutive-failures" : 4,\n  "delay" : 0,\n'
         '  "interval" : 15,\n  "timeout" : 10,\n  "grace-period" : 120,\n  "gracePeriod" : 120\n}')
+
+
+def test_value_json_fast_path_matches_the_protobuf_json_mapping():
+    """specs.value_to_json short-cuts scalar/range values; it must emit exactly what the generic
+    protobuf JSON mapping does (persisted configs are compared byte for byte)."""
+    from dcos_commons_amd.mesos import protos as P
+    from dcos_commons_amd.specification.specs import ranges_value, scalar_value, value_to_json
+
+    cases = [scalar_value(0.1), scalar_value(256), scalar_value(0.0), ranges_value([(1, 2), (10, 20)]),
+             ranges_value([]), ranges_value([(0, 2 ** 63)]), P.Value(type=P.Value.SCALAR),
+             P.Value(type=P.Value.RANGES), P.Value()]
+    s = P.Value(type=P.Value.SET)
+    s.set.item.extend(["a", "b"])
+    t = P.Value(type=P.Value.TEXT)
+    t.text.value = "x"
+    for v in cases + [s, t]:
+        assert value_to_json(v) == P.to_json(v), v
