@@ -236,13 +236,13 @@ class SchedulerConfig:
         return self.env.get_optional_double("SDK_OFFER_WAIT_S", 5.0)
 
     def gil_switch_interval_s(self) -> float:
-        """Interpreter thread switch interval for the scheduler process (``SDK_GIL_SWITCH_INTERVAL_MS``,
-        default 20 ms; 0 keeps the interpreter's 5 ms). The offer loop, the status path and the API
-        threads share one interpreter lock: with the 5 ms default a CPU-bound offer cycle is cut into
-        slices by every status arriving mid-cycle, and each hand-off back costs up to a full slice.
-        A longer interval lets a cycle finish and hands over at the natural blocking points (queue
-        waits, socket reads). Measured on the 8-agent deploy: 58 ms -> 41 ms (no change at 1 agent)."""
-        return self.env.get_optional_int("SDK_GIL_SWITCH_INTERVAL_MS", 20) / 1000.0
+        """Interpreter thread switch interval for the scheduler process (``SDK_GIL_SWITCH_INTERVAL_MS``;
+        default 0 = keep the interpreter's 5 ms). The offer loop, the status path and the API threads
+        share one interpreter lock. A longer interval lets an offer cycle finish before a status is
+        handled; unpinned, that took an 8-agent deploy from 58 to 41 ms on a slow CPU, but with the
+        process pinned to a few cores (bench.py) it only added tail latency (8-pod deploys with
+        22-37 ms outliers against <= 16 ms at 5 ms, profiles/ab_gil_interval_pinned_r03.txt)."""
+        return self.env.get_optional_int("SDK_GIL_SWITCH_INTERVAL_MS", 0) / 1000.0
 
     def is_revive_only_unmatched(self) -> bool:
         """Skip the REVIVE that new work asked for when the same offer cycle matched all of it
