@@ -14,6 +14,7 @@ rules.
 from __future__ import annotations
 
 import logging
+import os
 import sys
 from typing import Callable, Optional, Set
 
@@ -96,6 +97,12 @@ class FrameworkRunner:
         switch_s = self.scheduler_config.gil_switch_interval_s()
         if switch_s > 0:
             sys.setswitchinterval(switch_s)
+        cpus = self.scheduler_config.cpu_set()
+        if cpus:
+            try:
+                os.sched_setaffinity(0, cpus)   # threads started from here on inherit it
+            except (AttributeError, OSError) as e:
+                LOGGER.warning("Unable to pin the scheduler to CPUs %s: %s", cpus, e)
         framework_store = FrameworkStore(persister)
         self.framework_scheduler = FrameworkScheduler(self.resource_roles(), self.scheduler_config, persister,
                                                       framework_store, client)

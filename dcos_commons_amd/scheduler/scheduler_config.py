@@ -21,6 +21,23 @@ def _scalar(v: float) -> P.Value:
     return val
 
 
+def parse_cpu_list(text: str) -> list:
+    """``"0-3,8,10-11"`` -> ``[0, 1, 2, 3, 8, 10, 11]`` (Linux cpu-list syntax)."""
+    cpus = set()
+    for part in text.split(","):
+        part = part.strip()
+        if not part:
+            continue
+        lo, sep, hi = part.partition("-")
+        a, b = int(lo), int(hi) if sep else int(lo)
+        if a < 0 or b < a:
+            raise ValueError(f"Invalid cpu range '{part}' in '{text}'")
+        cpus.update(range(a, b + 1))
+    if not cpus:
+        raise ValueError(f"Empty cpu list '{text}'")
+    return sorted(cpus)
+
+
 class SchedulerConfig:
     _printed_build_info = False
 
@@ -243,6 +260,15 @@ class SchedulerConfig:
         process pinned to a few cores (bench.py) it only added tail latency (8-pod deploys with
         22-37 ms outliers against <= 16 ms at 5 ms, profiles/ab_gil_interval_pinned_r03.txt)."""
         return self.env.get_optional_int("SDK_GIL_SWITCH_INTERVAL_MS", 0) / 1000.0
+
+    def cpu_set(self) -> Optional[list]:
+        """CPUs the scheduler process runs on (``SDK_CPU_SET``, a Linux cpu list such as ``4-7`` or
+        ``2,3,8-9``; unset = wherever the OS puts it). Applied when the framework starts, so every
+        scheduler thread inherits it: the offer loop, status path and API threads hand work to each
+        other, and on a few warm cores those hand-offs do not wait for an idle core to wake
+        (bench.py pins its ranks the same way: deploy 4.2-5.1 -> 2.8 ms on the box)."""
+        v = self.env.get_optional("SDK_CPU_SET", "").strip()
+        return parse_cpu_list(v) if v else None
 
     def is_revive_only_unmatched(self) -> bool:
         """Skip the REVIVE that new work asked for when the same offer cycle matched all of it

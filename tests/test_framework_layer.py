@@ -551,3 +551,15 @@ def test_scheduler_process_switch_interval_flag():
     assert SchedulerConfig.for_testing().gil_switch_interval_s() == 0.0      # the interpreter's 5 ms
     assert SchedulerConfig.for_testing(SDK_GIL_SWITCH_INTERVAL_MS=20).gil_switch_interval_s() == 0.02
     assert sys.getswitchinterval() > 0
+
+
+def test_cpu_set_flag():
+    from dcos_commons_amd.scheduler.scheduler_config import SchedulerConfig, parse_cpu_list
+
+    assert parse_cpu_list("0-3,8,10-11") == [0, 1, 2, 3, 8, 10, 11]
+    assert parse_cpu_list(" 5 ") == [5]
+    for bad in ("", "3-1", "-1", "a"):
+        with pytest.raises(ValueError):
+            parse_cpu_list(bad)
+    assert SchedulerConfig.for_testing().cpu_set() is None
+    assert SchedulerConfig.for_testing(SDK_CPU_SET="2,3").cpu_set() == [2, 3]
