@@ -80,13 +80,34 @@ class FrameworkBench:
         self.timeout_s = timeout_s
 
     # -- helpers ---------------------------------------------------------------------------
-    def _wait(self, pred, what: str) -> float:
+    def _wait(self, pred, what: str, event=None) -> float:
+        """Until ``pred()``; with the scheduler's status-processed ``event`` the predicate is
+        re-checked when a status lands (and every 5 ms), as in ``DeployBench._wait``."""
         t0 = time.perf_counter()
-        while not pred():
+        while True:
+            if event is not None:
+                event.clear()
+            if pred():
+                return time.perf_counter() - t0
             if time.perf_counter() - t0 > self.timeout_s:
                 raise TimeoutError(f"timed out after {self.timeout_s}s waiting for {what}")
-            time.sleep(0.001)
-        return time.perf_counter() - t0
+            if event is not None:
+                event.wait(0.005)
+            else:
+                time.sleep(0.001)
+
+    @staticmethod
+    def _plan_done(scheduler, name: str) -> bool:
+        """What ``GET /v1/plans/<name>`` answers 200 for, read from the plan itself (rendering the
+        plan JSON on every poll competed with the scheduler being timed)."""
+        plan = scheduler.get_plan(name)
+        return plan is not None and not plan.has_errors() and plan.is_complete()
+
+    @staticmethod
+    def _expect_api(api, name: str) -> None:
+        r = api.get(f"/v1/plans/{name}")
+        if r.status != 200:
+            raise RuntimeError(f"/v1/plans/{name} answered {r.status} after the plan completed")
 
     def _config(self) -> SchedulerConfig:
         overrides = dict(PROFILES[self.profile])
@@ -138,8 +159,11 @@ class FrameworkBench:
             t0 = time.perf_counter()
             runner = self._start(master, env, cfg, persister)
             api, store = runner.framework_runner.api_server.router, runner.scheduler.state_store
-            self._wait(lambda: api.get("/v1/plans/deploy").status == 200, "cassandra deploy COMPLETE")
+            sched = runner.scheduler
+            ev = sched.status_processed
+            self._wait(lambda: self._plan_done(sched, "deploy"), "cassandra deploy COMPLETE", ev)
             deploy_s = time.perf_counter() - t0
+            self._expect_api(api, "deploy")
             rm = runner.framework_runner.framework_scheduler.offer_processor.revive_manager
             self._wait(lambda: rm.is_suppressed, "scheduler idle after deploy")
 
@@ -150,8 +174,9 @@ class FrameworkBench:
             if r.status != 200:
                 raise RuntimeError(f"replace failed: {r.status} {r.payload()!r}")
             self._wait(lambda: self._ready(store, "node-1-server", old) and
-                       api.get("/v1/plans/recovery").status == 200, "cassandra replace recovery")
+                       self._plan_done(sched, "recovery"), "cassandra replace recovery", ev)
             replace_s = time.perf_counter() - t1
+            self._expect_api(api, "recovery")
             cmd = store.fetch_task("node-1-server").command.value
             if "-Dcassandra.replace_address=" not in cmd:
                 raise RuntimeError("replacement did not go through CassandraRecoveryPlanOverrider")
@@ -173,8 +198,10 @@ class FrameworkBench:
             t0 = time.perf_counter()
             runner = self._start(master, env, cfg, persister)
             api = runner.framework_runner.api_server.router
-            self._wait(lambda: api.get("/v1/plans/deploy").status == 200, "hdfs deploy COMPLETE")
+            sched = runner.scheduler
+            self._wait(lambda: self._plan_done(sched, "deploy"), "hdfs deploy COMPLETE", sched.status_processed)
             deploy_s = time.perf_counter() - t0
+            self._expect_api(api, "deploy")
             store = runner.scheduler.state_store
             # the scheduler records deploy completion on its next status pass; a later config
             # change is then rolled out by the update plan instead of re-running deploy
@@ -194,9 +221,12 @@ class FrameworkBench:
             if plan is None or [p.get_name() for p in plan.get_children()] != ["journal", "name", "data"]:
                 raise RuntimeError("update plan was not selected for the configuration change: %r" % (
                     plan and [p.get_name() for p in plan.get_children()],))
-            self._wait(lambda: api.get("/v1/plans/deploy").status == 200 and
-                       all(self._ready(store, n, old) for n, old in before.items()), "hdfs rolling update")
+            sched = runner.scheduler
+            self._wait(lambda: self._plan_done(sched, "deploy") and
+                       all(self._ready(store, n, old) for n, old in before.items()), "hdfs rolling update",
+                       sched.status_processed)
             update_s = time.perf_counter() - t1
+            self._expect_api(api, "deploy")
             tasks = len(before)
         finally:
             if runner is not None:
