@@ -97,6 +97,7 @@ class DefaultScheduler(AbstractScheduler):
         self.deployment_plan_manager = next(pm for pm in pms if pm.get_plan().is_deploy_plan())
         self.recovery_plan_manager = next(pm for pm in pms if pm.get_plan().is_recovery_plan())
         self._deployment_completion_stored = False
+        self._expected_ids_cache: Dict[str, tuple] = {}   # task name -> (TaskInfo bytes, resource IDs, perm-failed)
         self.offer_outcome_tracker = None if namespace else OfferOutcomeTracker()
         self.offer_outcome_tracker_v2 = None if namespace else OfferOutcomeTrackerV2()
         if template_url_factory is None:
@@ -226,14 +227,32 @@ class DefaultScheduler(AbstractScheduler):
             # nothing reserved by this SDK in the leftover offers: no need to load every task to
             # learn which reservations are still expected
             return UnexpectedResourcesResponse.processed([])
+        offered = {rid for offer in unused_offers for r in offer.resources
+                   for rid in (get_resource_id(r),) if rid is not None}
         try:
+            # Only the expected IDs that appear in the offers decide anything, so a task whose
+            # reservations are not offered is skipped before its goal override is read; each
+            # task's IDs are memoized on its exact stored bytes (an unchanged TaskInfo is not
+            # parsed again on every offer cycle).
             keep = set()
-            for t in self.state_store.fetch_tasks():
-                if is_permanently_failed(t):
+            cache = self._expected_ids_cache
+            names = self.state_store.fetch_tasks_bytes()
+            for name, data in names.items():
+                hit = cache.get(name)
+                if hit is None or hit[0] != data:
+                    t = P.TaskInfo()
+                    t.ParseFromString(data)
+                    hit = cache[name] = (data, frozenset(get_resource_ids(get_all_resources(t))),
+                                         is_permanently_failed(t))
+                _, ids, failed = hit
+                if failed or ids.isdisjoint(offered):
                     continue
-                if self.state_store.fetch_goal_override_status(t.name) == DECOMMISSIONING_STATUS:
+                if self.state_store.fetch_goal_override_status(name) == DECOMMISSIONING_STATUS:
                     continue
-                keep.update(get_resource_ids(get_all_resources(t)))
+                keep.update(ids)
+            if len(cache) > len(names):
+                for gone in set(cache) - set(names):
+                    del cache[gone]
         except Exception:  # noqa: BLE001
             self.logger.exception("Failed to fetch expected tasks to determine unexpected resources")
             return UnexpectedResourcesResponse.failed([])

@@ -147,23 +147,50 @@ class StateStore:
                 return []
             raise StateStoreException(e.reason, str(e)) from e
 
-    def fetch_tasks(self) -> List[P.TaskInfo]:
-        out = []
-        for name in self.fetch_task_names():
-            t = self.fetch_task(name)
-            if t is None:
+    def fetch_tasks_bytes(self) -> Dict[str, bytes]:
+        """Every task's serialized TaskInfo by name, read in one persister call."""
+        names = self.fetch_task_names()
+        paths = {self._task_info_path(n): n for n in names}
+        try:
+            raw = self.persister.get_many(list(paths))
+        except PersisterException as e:
+            raise StateStoreException(e.reason, "Failed to retrieve tasks") from e
+        out = {}
+        for path, name in paths.items():
+            data = raw.get(path)
+            if data is None:
                 raise StateStoreException(
                     Reason.NOT_FOUND, f"Expected task named {name} to be present when retrieving all tasks")
+            if not data:
+                raise StateStoreException(Reason.SERIALIZATION_ERROR, f"Empty TaskInfo for TaskName: {name}")
+            out[name] = data
+        return out
+
+    def fetch_tasks(self) -> List[P.TaskInfo]:
+        out = []
+        for name, data in self.fetch_tasks_bytes().items():
+            t = P.TaskInfo()
+            try:
+                t.ParseFromString(data)
+            except Exception as e:  # noqa: BLE001
+                raise StateStoreException(Reason.SERIALIZATION_ERROR, str(e)) from e
             out.append(t)
         return out
 
-    def fetch_task(self, task_name: str) -> Optional[P.TaskInfo]:
+    def fetch_task_bytes(self, task_name: str) -> Optional[bytes]:
+        """The serialized TaskInfo as stored (None when absent), for callers that memoize what
+        they derive from a task on its exact bytes instead of parsing it on every pass."""
         try:
-            data = self.persister.get(self._task_info_path(task_name))
+            return self.persister.get(self._task_info_path(task_name))
         except PersisterException as e:
             if e.reason == Reason.NOT_FOUND:
                 return None
             raise StateStoreException(e.reason, f"Failed to retrieve task named {task_name}") from e
+
+    def fetch_task(self, task_name: str) -> Optional[P.TaskInfo]:
+        data = self.fetch_task_bytes(task_name)
+        if data is None:
+            return None
         if not data:
             raise StateStoreException(Reason.SERIALIZATION_ERROR, f"Empty TaskInfo for TaskName: {task_name}")
         t = P.TaskInfo()

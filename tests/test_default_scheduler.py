@@ -413,6 +413,25 @@ def test_unexpected_resources_of_failed_or_decommissioning_tasks(h, mark):
     assert list(resp.offer_resources[0].resources) == list(info.resources)
 
 
+def test_unexpected_resources_follow_cleared_and_rewritten_tasks(h):
+    """The per-task resource-ID memo is keyed on the stored bytes: clearing a task (or storing it
+    again without reservations) turns its offered reservations unexpected on the next pass."""
+    h.install()
+    store = StateStore(h.persister)
+    info = store.fetch_tasks()[0]
+    assert _unexpected(h, info.resources).offer_resources == []
+    bare = P.TaskInfo()
+    bare.CopyFrom(info)
+    del bare.resources[:]
+    store.store_tasks([bare])
+    assert list(_unexpected(h, info.resources).offer_resources[0].resources) == list(info.resources)
+    store.store_tasks([info])
+    assert _unexpected(h, info.resources).offer_resources == []
+    store.clear_task(info.name)
+    assert list(_unexpected(h, info.resources).offer_resources[0].resources) == list(info.resources)
+    assert info.name not in h.scheduler._expected_ids_cache
+
+
 def test_unexpected_resources_of_unknown_reservations(h):
     h.install()
     stray = U.reserved_cpus(1.0, "not-a-known-resource")
