@@ -154,6 +154,9 @@ class FrameworkScheduler:
             LOGGER.info("Received status update for taskId=%s state=%s message='%s'", status.task_id.value,
                         P.TaskState.Name(status.state), status.message)
             metrics.record_status(status)
+            # a status during explicit reconciliation may end it: wake the loop whatever the state
+            awaiting = getattr(self.client, "awaiting_reconciliation", None)
+            reconciling = awaiting is not None and awaiting()
             with trace.span("status", "status", task=status.task_id.value, state=P.TaskState.Name(status.state)):
                 resp = self.client.task_status(status)
             eligible = task_killer.update(status)
@@ -165,7 +168,7 @@ class FrameworkScheduler:
                 else:
                     LOGGER.warning("Received status update for unknown task, but task should not be killed "
                                    "again: %s", status.task_id.value)
-            if resp.result == TaskStatusResult.UNKNOWN_TASK or can_create_work(status):
+            if resp.result == TaskStatusResult.UNKNOWN_TASK or reconciling or can_create_work(status):
                 self.offer_processor.kick()
         except Exception as e:  # noqa: BLE001
             self._exit(e)

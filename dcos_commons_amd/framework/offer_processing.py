@@ -440,8 +440,11 @@ class OfferProcessor:
         self.merge_agent_offers = merge_agent_offers
         # ACCEPT each step's launch as soon as it is matched instead of after the whole cycle
         self.stream_launches = stream_launches
-        # drop a revive requested for new work when that work was matched in the same cycle
-        self.revive_only_unmatched = revive_only_unmatched
+        # drop a revive requested for new work when that work was matched in the same cycle. Only
+        # with held offers: with hold_s == 0 the cycle's leftovers were long-declined, and that
+        # revive is what clears their filters for a later relaunch of the same step (which adds no
+        # new work and so asks for no revive of its own)
+        self.revive_only_unmatched = revive_only_unmatched and hold_s > 0
         # (real) offer id -> (offer, hold deadline). Rescinds arrive on the driver's thread while
         # the offer thread evaluates, so the map is only touched under _held_lock, and an offer
         # rescinded mid-cycle is remembered so that the cycle does not hold it again.

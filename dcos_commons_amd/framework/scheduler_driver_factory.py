@@ -83,10 +83,26 @@ class SchedulerDriverFactory:
         return LocalSchedulerDriver(local_master_from_env(scheduler_config.env), scheduler, framework_info)
 
 
+def check_principal_override(framework_info: P.FrameworkInfo, scheduler_config) -> None:
+    """The credential's principal is always ``FrameworkInfo.principal`` (the master rejects a
+    credential for another principal). ``SDK_MESOS_PRINCIPAL`` names the principal of hand-built
+    drivers (``SchedulerConfig.mesos_credential``); set to a different value for the scheduler it
+    would be silently ignored, so that is refused as a configuration error instead."""
+    override = scheduler_config.env.get_optional("SDK_MESOS_PRINCIPAL", "")
+    if override and override != framework_info.principal:
+        raise ValueError(f"SDK_MESOS_PRINCIPAL={override!r} differs from the framework principal "
+                         f"{framework_info.principal!r}; the scheduler authenticates as the framework principal "
+                         f"(set FRAMEWORK_PRINCIPAL / service.principal instead)")
+
+
 def default_driver_factory(scheduler_config) -> Callable:
     """``driver_factory(scheduler, framework_info)`` for FrameworkRunner."""
     factory = SchedulerDriverFactory()
     master = scheduler_config.mesos_master_url()
     secret = scheduler_config.env.get_optional("SDK_MESOS_SECRET", "")
-    return lambda sched, info: factory.create(sched, info, master, scheduler_config,
-                                              secret.encode("utf-8") if secret else None)
+
+    def create(sched, info):
+        check_principal_override(info, scheduler_config)
+        return factory.create(sched, info, master, scheduler_config, secret.encode("utf-8") if secret else None)
+
+    return create

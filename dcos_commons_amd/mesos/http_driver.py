@@ -206,7 +206,11 @@ class V1HttpSchedulerDriver(SchedulerDriver):
     def _headers(self, accept: str) -> dict:
         h = {"Content-Type": self.content_type, "Accept": accept, "Connection": "keep-alive"}
         if self.token_provider is not None:
-            tok = self.token_provider()
+            try:
+                tok = self.token_provider()
+            except Exception as e:  # noqa: BLE001 -- IAM outage, bad credential, parse error...
+                # status 0 = transport failure: SUBSCRIBE retries with backoff, calls retry below
+                raise MesosCallError(0, f"auth token refresh failed: {type(e).__name__}: {e}") from e
             h["Authorization"] = "token=" + (tok.value if hasattr(tok, "value") else str(tok))
         elif self.credential is not None and self.credential.principal:
             token = f"{self.credential.principal}:{self.credential.secret or ''}".encode("utf-8")
@@ -233,9 +237,18 @@ class V1HttpSchedulerDriver(SchedulerDriver):
         if self.stream_id is None:
             raise MesosCallError(0, f"not subscribed; dropping {P.Call.Type.Name(call.type)}")
         body = encode_message(call, self.content_type)
+        backoff = self.backoff_s
         for attempt in range(3):
             conn = self._thread_conn()
-            headers = self._headers(self.content_type)
+            try:
+                headers = self._headers(self.content_type)
+            except MesosCallError as e:
+                if attempt == 2 or self._stopped.is_set():
+                    raise
+                LOGGER.warning("%s: retrying %s in %.1fs", e, P.Call.Type.Name(call.type), backoff)
+                self._stopped.wait(backoff)
+                backoff = min(backoff * 2, self.max_backoff_s)
+                continue
             headers[STREAM_ID_HEADER] = self.stream_id
             try:
                 conn.request("POST", SCHEDULER_PATH, body=body, headers=headers)

@@ -188,7 +188,8 @@ def readiness(device: int = 0, seed: int = 0, inject: int = 0):
     """The whole readiness check of one device in one native call (no framework ops): hashed bf16
     operands, the MFMA GEMM, a dense fp32 check of every product element and the 64 MiB HBM
     pattern test on a private stream, then one 32-byte read-back. Returns ``(gemm_rel_err, bad_words)``. ``inject`` = 1 or
-    2 plants a product / memory fault (tests). The GIL is released for the duration (ctypes)."""
+    2 plants a product / memory fault, 3 / 4 skips the GEMM / pattern write (tests). Each call mixes
+    a call counter into ``seed``, so stale buffers from an earlier call never verify. The GIL is released for the duration (ctypes)."""
     rel = ctypes.c_double(0.0)
     bad = ctypes.c_ulonglong(0)
     _check(lib().amdprobe_readiness(int(device), seed & 0xFFFFFFFF, int(inject), ctypes.byref(rel),

@@ -107,7 +107,14 @@ AMDPROBE_EXPORT int amdprobe_readiness_fill(void* ab, size_t ab_bytes, unsigned 
 // Buffers, a non-blocking stream and a pinned result slot are created on first use per device
 // and reused; calls for one device serialize on its context. The calling thread's current device
 // is restored. inject: 0 = none, 1 = lose one 16x16 tile of the product (the check must fail), 2 = corrupt one
-// pattern word (the memory check must count it). Returns 0 or a HIP error / negative shape code.
+// pattern word (the memory check must count it), 3 = skip the GEMM launch, 4 = skip the pattern write (both
+// model a kernel that silently drops its writes; the check must still fail). Returns 0 or a HIP error /
+// negative shape code.
+//
+// The buffers outlive the call, so a kernel that dropped its writes would leave the previous call's correct
+// data behind. Two things stop that from passing: C is poisoned with NaN bytes before the GEMM, and every
+// call mixes a per-device call counter into the seed, so the operands and the pattern differ from the last
+// call's and stale data cannot match.
 // ---------------------------------------------------------------------------------------
 namespace {
 constexpr int RM = 256, RN = 256, RK = 512;
@@ -123,6 +130,7 @@ struct ReadinessCtx {
   uint4* pattern = nullptr;
   ReadinessResult* res = nullptr;
   ReadinessResult* host = nullptr;  // pinned
+  uint32_t calls = 0;               // mixed into the seed: no two calls share operands or pattern
 };
 ReadinessCtx g_readiness[MAX_DEVICES];
 
@@ -197,26 +205,32 @@ AMDPROBE_EXPORT int amdprobe_readiness(int device, unsigned seed, int inject, do
   hipStream_t s = ctx.stream;
   const __bf16* A = ctx.ab;
   const __bf16* Bt = ctx.ab + size_t(RM) * RK;
+  const uint32_t call_seed = (uint32_t)seed ^ (0x9E3779B9u * ++ctx.calls);
   hipLaunchKernelGGL(readiness_prep_kernel, dim3(64), dim3(256), 0, s, (uint4*)ctx.ab,
-                     size_t(RM + RN) * RK * sizeof(__bf16) / 16, (uint32_t)seed, ctx.res);
+                     size_t(RM + RN) * RK * sizeof(__bf16) / 16, call_seed, ctx.res);
   PROBE_TRY(hipGetLastError());
-  // 128x128 tiles: four workgroups for the 256x256 product (one 256x256-tile workgroup takes ~15 us)
-  const int rc = amdprobe_gemm_bf16_nt_variant(A, Bt, ctx.c, RM, RN, RK, 1, s);
-  if (rc) return rc;
+  PROBE_TRY(hipMemsetAsync(ctx.c, 0xFF, size_t(RM) * RN * sizeof(float), s));  // NaN until the GEMM writes
+  if (inject != 3) {
+    // 128x128 tiles: four workgroups for the 256x256 product (one 256x256-tile workgroup takes ~15 us)
+    const int rc = amdprobe_gemm_bf16_nt_variant(A, Bt, ctx.c, RM, RN, RK, 1, s);
+    if (rc) return rc;
+  }
   hipLaunchKernelGGL(gemm_check_kernel, dim3((RM / CHECK_TILE) * (RN / CHECK_TILE)), dim3(CHECK_THREADS), 0, s, A,
                      Bt, (const float*)ctx.c, RM, RN, RK, inject == 1 ? 1 : 0, &ctx.res->diff2);
   PROBE_TRY(hipGetLastError());
-  hipLaunchKernelGGL(pattern_write_kernel, dim3(2048), dim3(256), 0, s, ctx.pattern, PATTERN_BYTES / 16,
-                     (uint32_t)seed);
-  PROBE_TRY(hipGetLastError());
+  if (inject != 4) {
+    hipLaunchKernelGGL(pattern_write_kernel, dim3(2048), dim3(256), 0, s, ctx.pattern, PATTERN_BYTES / 16,
+                       call_seed);
+    PROBE_TRY(hipGetLastError());
+  }
   if (inject == 2) PROBE_TRY(hipMemsetAsync(ctx.pattern, 0, 4, s));
   hipLaunchKernelGGL(pattern_check_kernel, dim3(2048), dim3(256), 0, s, (const uint4*)ctx.pattern,
-                     PATTERN_BYTES / 16, (uint32_t)seed, &ctx.res->bad_words);
+                     PATTERN_BYTES / 16, call_seed, &ctx.res->bad_words);
   PROBE_TRY(hipGetLastError());
   PROBE_TRY(hipMemcpyAsync(ctx.host, ctx.res, sizeof(ReadinessResult), hipMemcpyDeviceToHost, s));
   PROBE_TRY(hipStreamSynchronize(s));
   const double d2 = ctx.host->diff2, w2 = ctx.host->ref2;
-  *rel_err = w2 > 0.0 ? std::sqrt(d2 / w2) : HUGE_VAL;
+  *rel_err = (w2 > 0.0 && std::isfinite(d2)) ? std::sqrt(d2 / w2) : HUGE_VAL;  // NaN C (never written) fails
   *bad_words = ctx.host->bad_words;
   return 0;
 }

@@ -133,6 +133,9 @@ class AbstractScheduler(MesosEventClient):
             self.status_processed.set()
         return TaskStatusResponse.processed()
 
+    def awaiting_reconciliation(self) -> bool:
+        return self.reconciler is None or not self.reconciler.is_reconciled()
+
     # abstract
     def registered_with_mesos(self) -> None:
         raise NotImplementedError

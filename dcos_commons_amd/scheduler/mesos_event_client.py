@@ -178,6 +178,13 @@ class MesosEventClient:
     def task_status(self, status: P.TaskStatus) -> TaskStatusResponse:
         raise NotImplementedError
 
+    def awaiting_reconciliation(self) -> bool:
+        """True while explicit reconciliation has not finished. Offers are refused until then, so
+        every status that arrives in that window may be the one that ends it, and the framework
+        wakes the offer loop for each of them whatever its state (no reference counterpart: the
+        reference's offer loop only polls)."""
+        return False
+
     def get_http_endpoints(self):
         """Returns a list of ``dcos_commons_amd.http`` route providers."""
         return []

@@ -419,6 +419,9 @@ class MultiServiceEventClient(MesosEventClient):
         vals = list(unexpected.values())
         return UnexpectedResourcesResponse.failed(vals) if failed else UnexpectedResourcesResponse.processed(vals)
 
+    def awaiting_reconciliation(self) -> bool:
+        return any(s.awaiting_reconciliation() for s in self.manager.all_services())
+
     def task_status(self, status) -> TaskStatusResponse:
         s = self.manager.get_matching_service(status)
         if s is None:

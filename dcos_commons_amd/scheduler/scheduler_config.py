@@ -273,7 +273,9 @@ class SchedulerConfig:
     def is_revive_only_unmatched(self) -> bool:
         """Skip the REVIVE that new work asked for when the same offer cycle matched all of it
         (``SDK_REVIVE_ONLY_UNMATCHED``; reference: revive on every work-set change). The revive
-        would only bring this cycle's leftovers back for another evaluation pass."""
+        would only bring this cycle's leftovers back for another evaluation pass. Applies only with
+        ``SDK_OFFER_HOLD_S`` > 0: without held offers the leftovers are declined for an hour, and
+        the revive is what clears those decline filters for a later relaunch of the same step."""
         return self.env.get_optional_boolean("SDK_REVIVE_ONLY_UNMATCHED", True)
 
     def is_event_driven(self) -> bool:

@@ -319,6 +319,9 @@ class UninstallScheduler:
                 self._recheck = True
         return OfferResponse.processed([])
 
+    def awaiting_reconciliation(self) -> bool:
+        return self.reconciler is None or not self.reconciler.is_reconciled()
+
     def consume_recheck_request(self) -> bool:
         """True once after the deregister step started: the offer loop re-checks the client
         status immediately and tears the framework down without waiting for the next poll."""

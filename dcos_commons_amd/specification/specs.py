@@ -15,6 +15,7 @@ Protobuf ``Value`` fields are serialized with the protobuf JSON mapping.
 from __future__ import annotations
 
 import enum
+import functools
 import json
 import re
 from dataclasses import dataclass, field, replace
@@ -1045,19 +1046,12 @@ class ServiceSpec:
         return ServiceSpec.from_dict(json.loads(data.decode("utf-8")))
 
 
-_PARSED_SPECS: Dict[bytes, "ServiceSpec"] = {}
-_PARSED_SPECS_MAX = 32
-
-
+@functools.lru_cache(maxsize=32)
 def _parse_cached(data: bytes) -> "ServiceSpec":
-    """JSON -> ServiceSpec, memoized by the exact bytes (specs are immutable, parsing is pure)."""
-    spec = _PARSED_SPECS.get(data)
-    if spec is None:
-        spec = ServiceSpec.from_json_bytes(data)
-        if len(_PARSED_SPECS) >= _PARSED_SPECS_MAX:
-            _PARSED_SPECS.pop(next(iter(_PARSED_SPECS)))
-        _PARSED_SPECS[data] = spec
-    return spec
+    """JSON -> ServiceSpec, memoized by the exact bytes (specs are immutable, parsing is pure).
+    ``lru_cache`` is thread-safe: services of a multi-service scheduler run their loopback checks
+    concurrently."""
+    return ServiceSpec.from_json_bytes(data)
 
 
 class ServiceSpecFactory:

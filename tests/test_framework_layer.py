@@ -416,6 +416,55 @@ def test_foreign_reservations_are_filtered(drv):
     assert [r.name for r in got[0].resources] == ["cpus"]
 
 
+class _ReconcilingClient(_StatusClient):
+    """Explicit reconciliation is pending until the first status arrives."""
+
+    def __init__(self):
+        super().__init__(known={"t"})
+        self.reconciled = False
+
+    def awaiting_reconciliation(self):
+        return not self.reconciled
+
+    def task_status(self, status):
+        resp = super().task_status(status)
+        self.reconciled = True
+        return resp
+
+
+def test_status_that_ends_reconciliation_wakes_the_offer_loop(drv):
+    """A TASK_STARTING cannot create work on its own (can_create_work is False), but when it is the
+    status that ends explicit reconciliation the offer loop must run now: offers were refused until
+    then, and without the kick they would wait for the next offer or the 5 s poll."""
+    c = _ReconcilingClient()
+    fs, _ = _fs(c)
+    kicks = []
+    fs.offer_processor.kick = lambda: kicks.append(1)
+    starting = P.TaskStatus(task_id=P.TaskID(value="t"), state=P.TASK_STARTING)
+    fs.status_update(drv, starting)
+    assert kicks == [1]
+    fs.status_update(drv, starting)          # reconciled: a STARTING no longer wakes the loop
+    assert kicks == [1]
+
+
+def test_abstract_scheduler_reports_reconciliation_progress():
+    from dcos_commons_amd.scheduler.abstract_scheduler import AbstractScheduler
+
+    class _Reconciler:
+        done = False
+
+        def is_reconciled(self):
+            return self.done
+
+    s = AbstractScheduler.__new__(AbstractScheduler)
+    s.reconciler = None
+    assert s.awaiting_reconciliation()                    # not registered yet
+    s.reconciler = _Reconciler()
+    assert s.awaiting_reconciliation()
+    s.reconciler.done = True
+    assert not s.awaiting_reconciliation()
+
+
 def test_unknown_task_status_kills_once(drv):
     c = _StatusClient(known={"known"})
     fs, _ = _fs(c)
@@ -529,15 +578,17 @@ class _Step:
         return False
 
 
-@pytest.mark.parametrize("flag,pending,revives", [
-    (True, False, 0),    # the new work launched from offers in hand: no revive
-    (True, True, 1),     # a candidate is still unmatched: revive for more offers
-    (False, False, 1),   # reference: every new work set revives
+@pytest.mark.parametrize("flag,pending,hold_s,revives", [
+    (True, False, 10.0, 0),    # the new work launched from offers in hand: no revive
+    (True, True, 10.0, 1),     # a candidate is still unmatched: revive for more offers
+    (False, False, 10.0, 1),   # reference: every new work set revives
+    # no held offers: leftovers were long-declined, and this revive is what clears their filters
+    (True, False, 0.0, 1),
 ])
-def test_revive_only_for_unmatched_new_work(drv, flag, pending, revives):
+def test_revive_only_for_unmatched_new_work(drv, flag, pending, hold_s, revives):
     client = Client(status=ClientStatusResponse.launching(True))
     client.candidate_steps = [_Step(pending)]
-    p = processor(client, revive_only_unmatched=flag).disable_threading()
+    p = processor(client, revive_only_unmatched=flag, hold_s=hold_s).disable_threading()
     p.start()
     p.enqueue([offer("a")])
     assert drv.revives == revives

@@ -208,12 +208,19 @@ def test_fused_readiness_passes_and_catches_planted_faults(dev):
 
     rel, bad = ops.readiness(0, seed=4321)
     assert rel < 1e-4 and bad == 0
-    again = ops.readiness(0, seed=4321)               # same data; float atomics reorder the sums only
-    assert again[1] == 0 and again[0] == pytest.approx(rel, rel=0.2, abs=1e-9)
+    again = ops.readiness(0, seed=4321)               # fresh operands and pattern (call counter in the seed)
+    assert again[1] == 0 and again[0] < 1e-4
     rel1, bad1 = ops.readiness(0, seed=4321, inject=1)
     assert rel1 > MAX_GEMM_REL_ERR and bad1 == 0
     rel2, bad2 = ops.readiness(0, seed=4321, inject=2)
     assert rel2 < 1e-4 and bad2 >= 1
+    # a GEMM or pattern write that silently drops its stores must not pass on the previous call's data
+    rel3, bad3 = ops.readiness(0, seed=4321, inject=3)
+    assert rel3 > MAX_GEMM_REL_ERR and bad3 == 0
+    rel4, bad4 = ops.readiness(0, seed=4321, inject=4)
+    assert rel4 < 1e-4 and bad4 > 1000
+    rel5, bad5 = ops.readiness(0, seed=4321)                    # healthy again
+    assert rel5 < 1e-4 and bad5 == 0
     assert ops.readiness(0, seed=7)[1] == 0
     with pytest.raises(ops.ProbeError):
         ops.readiness(torch.cuda.device_count(), seed=1)

@@ -11,7 +11,7 @@ import pytest
 from dcos_commons_amd.framework.process_exit import ProcessExit
 from dcos_commons_amd.mesos import protos as P
 from dcos_commons_amd.mesos import recordio
-from dcos_commons_amd.mesos.http_driver import JSON, PROTOBUF, V1HttpSchedulerDriver, encode_message
+from dcos_commons_amd.mesos.http_driver import JSON, PROTOBUF, MesosCallError, V1HttpSchedulerDriver, encode_message
 from dcos_commons_amd.mesos.http_master import HttpMaster
 from dcos_commons_amd.mesos.local_master import AgentSpec, LocalMaster
 from test_e2e_helloworld import Cluster
@@ -362,3 +362,44 @@ def test_zk_master_detection(cluster):
         standby.stop()
     finally:
         zk.stop()
+
+
+def test_token_refresh_failures_take_the_retry_path(cluster):
+    """An IAM token refresh that fails (outage, bad credential) is a transport failure, not an
+    exception out of every driver call: SUBSCRIBE retries with backoff and calls retry, and the
+    driver carries on once the provider answers again."""
+    lm, hm = cluster
+    rec = Recorder()
+    failures = {"left": 2}
+
+    def provider():
+        if failures["left"] > 0:
+            failures["left"] -= 1
+            raise ConnectionError("IAM unavailable")
+        return "jwt"
+
+    d = V1HttpSchedulerDriver(hm.url, rec, P.FrameworkInfo(name="fw", role="r", principal="p"),
+                              credential=P.Credential(principal="p"), token_provider=provider, backoff_s=0.01)
+    d.start()
+    try:
+        rec.wait_for("registered")                  # two failed SUBSCRIBE attempts, then success
+        failures["left"] = 1
+        d.revive_offers()                           # one failed header build, retried
+        assert hm.calls["REVIVE"] == 1
+        failures["left"] = 5
+        with pytest.raises(MesosCallError) as e:
+            d.suppress_offers()                     # still failing after three attempts
+        assert e.value.status == 0 and "token refresh failed" in str(e.value)
+    finally:
+        d.stop()
+
+
+def test_mesos_principal_override_must_match_the_framework_principal():
+    from dcos_commons_amd.framework.scheduler_driver_factory import check_principal_override
+    from dcos_commons_amd.scheduler.scheduler_config import SchedulerConfig
+
+    info = P.FrameworkInfo(name="fw", principal="svc-principal")
+    check_principal_override(info, SchedulerConfig.for_testing())
+    check_principal_override(info, SchedulerConfig.for_testing(SDK_MESOS_PRINCIPAL="svc-principal"))
+    with pytest.raises(ValueError, match="SDK_MESOS_PRINCIPAL"):
+        check_principal_override(info, SchedulerConfig.for_testing(SDK_MESOS_PRINCIPAL="other"))

@@ -155,3 +155,25 @@ def test_helloworld_gpu_spec_requests_gpus():
     assert raw.plans["deploy"]["strategy"] == "parallel"
     t = spec.pods[0].tasks[0]
     assert t.readiness_check.command == "amd-gpu-probe --readiness"
+
+
+def test_loopback_parse_cache_is_thread_safe():
+    """The loopback parse cache is shared by every service of a multi-service scheduler; concurrent
+    checks that evict entries must neither raise nor return another spec's parse."""
+    from concurrent.futures import ThreadPoolExecutor
+    from dataclasses import replace
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {"FRAMEWORK_NAME": "hw", "FRAMEWORK_PRINCIPAL": "p", "FRAMEWORK_USER": "nobody", "HELLO_COUNT": "2",
+           "HELLO_PLACEMENT": '[["hostname", "UNIQUE"]]', "HELLO_CPUS": "0.1", "HELLO_GPUS": "1", "HELLO_MEM": "252",
+           "HELLO_DISK": "25", "SLEEP_DURATION": "1000", "GPU_PROBE_CMD": "amd-gpu-probe --readiness"}
+    _, base = build(os.path.join(root, "frameworks", "helloworld", "specs", "gpu.yml"), env)
+    specs = [replace(base, name=f"svc-{i}") for i in range(80)]       # more than the cache holds
+
+    def check(i):
+        s = specs[i % len(specs)]
+        assert S._parse_cached(s.to_json_bytes()) == s
+        return S.loopback_check(s) is not None
+
+    with ThreadPoolExecutor(8) as pool:
+        assert all(pool.map(check, range(800)))
