@@ -82,6 +82,9 @@ class DeployBench:
         self.allocation_interval_s = allocation_interval_s
         self.timeout_s = timeout_s
         self.agent_runners = agent_runners  # per-agent check runner (remote GPU agents)
+        # the agents' check executors outlive a cycle, as they outlive a scheduler on a real cluster
+        self.behavior = TaskBehavior(TaskTiming(), check_runner=self.check_runner,
+                                     check_workers=max(8, n_agents)).prestart()
 
     # -- helpers ---------------------------------------------------------------------------
     def _wait(self, pred, what: str, event=None) -> float:
@@ -129,8 +132,7 @@ class DeployBench:
             raise RuntimeError(f"/v1/plans/{plan} answered {r.status} after the plan completed")
 
     def _make_master(self) -> LocalMaster:
-        behavior = TaskBehavior(TaskTiming(), check_runner=self.check_runner)
-        master = LocalMaster(allocation_interval_s=self.allocation_interval_s, behavior=behavior)
+        master = LocalMaster(allocation_interval_s=self.allocation_interval_s, behavior=self.behavior)
         for i in range(self.n):
             dev = self.gpu_devices[i % len(self.gpu_devices)]
             master.add_agent(AgentSpec(hostname=f"mi355x-agent-{i}", cpus=16, mem=65536, disk=100000, gpus=1,

@@ -161,6 +161,19 @@ class TaskBehavior:
             self._pool = ThreadPoolExecutor(max_workers=self._workers, thread_name_prefix="task-check")
         return self._pool
 
+    def prestart(self) -> "TaskBehavior":
+        """Start every check worker now. An agent's check executor is already running when a task
+        launches; without this the pool starts a thread at each of the first checks, inside the
+        launch being timed."""
+        import threading as _threading
+
+        pool = self.pool()
+        gate = _threading.Barrier(self._workers + 1)
+        for _ in range(self._workers):
+            pool.submit(gate.wait, 10.0)
+        gate.wait(10.0)
+        return self
+
     def timing(self, task: P.TaskInfo) -> TaskTiming:
         for k, v in self.overrides.items():
             if k in task.name:

@@ -20,7 +20,7 @@ from dcos_commons_amd.state.goal_state_override import (
     OverrideStatus,
 )
 
-from .elements import AbstractStep
+from .elements import AbstractStep, bump_status_generation
 from .pod_instance_requirement import PodInstanceRequirement
 from .status import Status
 
@@ -57,6 +57,7 @@ class DeploymentStep(AbstractStep):
 
     def add_error(self, error: str) -> "DeploymentStep":
         self._errors.append(error)
+        bump_status_generation()
         self._update_status()
         return self
 

@@ -20,6 +20,27 @@ from .status import Status
 
 LOGGER = logging.getLogger(__name__)
 
+# ---------------------------------------------------------------------------------------
+# Status generation: bumped (under a lock, so it only ever grows) after every change that can
+# alter an aggregate status -- a step's status, its interrupted flag or its errors, a strategy's
+# interrupted flag. A phase/plan caches its aggregate together with the generation it read
+# *before* computing it, so a change that lands during the computation invalidates the entry.
+# Plan status is read far more often than it changes: every offer cycle's candidate walk, every
+# status update, every /v1/plans request and the plan-status metric.
+
+_status_gen = 0
+_status_gen_lock = threading.Lock()
+
+
+def bump_status_generation() -> None:
+    global _status_gen
+    with _status_gen_lock:
+        _status_gen += 1
+
+
+def status_generation() -> int:
+    return _status_gen
+
 
 # ---------------------------------------------------------------------------------------
 # PlanUtils
@@ -228,7 +249,31 @@ class ParentElement(Element):
     # instead of being reported as ERROR; a persistent one still is.
     _TORN_READ_RETRIES = 3
 
+    # (generation, status) of the last aggregate, when it may be reused (see _status_gen)
+    _status_cache = None
+    # whether the last computed aggregate was cacheable (read by the parent plan)
+    _last_cacheable = False
+
+    def _cacheable(self, children, child_statuses) -> bool:
+        """An aggregate may be reused until the generation moves when everything it read reports
+        its changes through the generation: AbstractStep children that are not DELAYED (a DELAYED
+        step turns PENDING by itself once its backoff expires), cacheable child phases, and a
+        deterministic strategy (RandomStrategy picks a different candidate on every call)."""
+        if not getattr(self.get_strategy(), "deterministic", False):
+            return False
+        for c, s in zip(children, child_statuses):
+            if isinstance(c, AbstractStep):
+                if s is Status.DELAYED or c._status is Status.DELAYED:
+                    return False
+            elif not (isinstance(c, ParentElement) and c._last_cacheable):
+                return False
+        return True
+
     def get_status(self) -> Status:
+        gen = _status_gen
+        cached = self._status_cache
+        if cached is not None and cached[0] == gen:
+            return cached[1]
         children = self.get_children()
         errors = self.get_errors()
         for attempt in range(self._TORN_READ_RETRIES + 1):
@@ -238,7 +283,10 @@ class ParentElement(Element):
             st = get_aggregate_status(self.get_name(), child_statuses, candidate_statuses, errors,
                                       self.is_interrupted(), log_unexpected=last)
             if st != Status.ERROR or errors or Status.ERROR in child_statuses or last:
-                return st
+                break
+        cacheable = self._cacheable(children, child_statuses)
+        self._last_cacheable = cacheable
+        self._status_cache = (gen, st) if cacheable else None
         return st
 
 
@@ -301,6 +349,7 @@ class AbstractStep(Step):
             old = self._status
             self._status = new_status
         if old != new_status:
+            bump_status_generation()
             self.logger.info("%s: changed status from: %s to: %s (interrupted=%s)", self._name, old, new_status,
                              self._interrupted)
 
@@ -309,14 +358,15 @@ class AbstractStep(Step):
     def interrupt(self) -> None:
         with self._status_lock:
             self._interrupted = True
+        bump_status_generation()
 
     def proceed(self) -> None:
         with self._status_lock:
             self._interrupted = False
+        bump_status_generation()
 
     def is_interrupted(self) -> bool:
-        with self._status_lock:
-            return self._interrupted
+        return self._interrupted        # a plain attribute read is atomic
 
     def restart(self) -> None:
         self.logger.warning("Restarting step: '%s [%s]'", self._name, self._id)

@@ -10,12 +10,16 @@ import random
 import threading
 from typing import Callable, Dict, Iterable, List, Optional
 
-from .elements import is_eligible
+from .elements import bump_status_generation, is_eligible
 
 DEFAULT_CANARY_PROCEED_COUNT = 2
 
 
 class Strategy:
+    # the same elements in the same states always give the same candidates (aggregate statuses
+    # computed through this strategy may be cached, see elements._status_gen)
+    deterministic = False
+
     def get_candidates(self, elements, dirty_assets) -> list:
         raise NotImplementedError
 
@@ -44,10 +48,12 @@ class InterruptibleStrategy(Strategy):
     def interrupt(self) -> None:
         with self._lock:
             self._interrupted = True
+        bump_status_generation()
 
     def proceed(self) -> None:
         with self._lock:
             self._interrupted = False
+        bump_status_generation()
 
     def is_interrupted(self) -> bool:
         return self._interrupted
@@ -84,6 +90,8 @@ class DependencyStrategyHelper:
 
 
 class SerialStrategy(InterruptibleStrategy):
+    deterministic = True
+
     def __init__(self):
         super().__init__()
         self._helper: Optional[DependencyStrategyHelper] = None
@@ -108,8 +116,13 @@ class SerialStrategy(InterruptibleStrategy):
 
 
 class ParallelStrategy(InterruptibleStrategy):
+    deterministic = True
+
     def get_candidates(self, elements, dirty_assets):
-        return DependencyStrategyHelper(elements).get_candidates(self.is_interrupted(), dirty_assets)
+        # a dependency helper with no edges: every eligible element, in order
+        if self._interrupted:
+            return []
+        return [e for e in elements if is_eligible(e, dirty_assets)]
 
     def get_name(self):
         return "parallel"
@@ -127,6 +140,8 @@ class RandomStrategy(InterruptibleStrategy):
 
 
 class DependencyStrategy(InterruptibleStrategy):
+    deterministic = True
+
     def __init__(self, helper: DependencyStrategyHelper):
         super().__init__()
         self.helper = helper
@@ -166,6 +181,10 @@ class CanaryStrategy(Strategy):
 
     def get_name(self):
         return self.strategy.get_name() + "-canary"
+
+    @property
+    def deterministic(self) -> bool:
+        return getattr(self.strategy, "deterministic", False)
 
     def interrupt(self) -> None:
         if self._next_canary_step() is not None:

@@ -51,26 +51,41 @@ class StateStore:
         self.persister = persister
         self.namespace = namespace or ""
         self.logger = logging.getLogger(__name__ + (f"({self.namespace})" if self.namespace else ""))
+        self._tasks_root = get_service_namespaced_root_path(self.namespace, TASKS_ROOT_NAME)
+        # task name -> (task, TaskInfo, TaskStatus, goal-override, override-status) paths: every
+        # offer cycle and status update reads these for every task
+        self._paths: Dict[str, tuple] = {}
         if repair:
             from .state_store_utils import repair_task_ids
 
             repair_task_ids(self)
 
     # -- paths ---------------------------------------------------------------------------
+    def _task_paths(self, name: str) -> tuple:
+        p = self._paths.get(name)
+        if p is None:
+            task = join_paths(self._tasks_root, name)
+            p = (task, join_paths(task, TASK_INFO_PATH_NAME), join_paths(task, TASK_STATUS_PATH_NAME),
+                 join_paths(task, TASK_METADATA_PATH_NAME, TASK_GOAL_OVERRIDE_PATH_NAME),
+                 join_paths(task, TASK_METADATA_PATH_NAME, TASK_GOAL_OVERRIDE_STATUS_PATH_NAME))
+            if len(self._paths) < 100000:      # bounded: task names come from pod specs
+                self._paths[name] = p
+        return p
+
     def _task_path(self, task_name: str) -> str:
-        return join_paths(get_service_namespaced_root_path(self.namespace, TASKS_ROOT_NAME), task_name)
+        return self._task_paths(task_name)[0]
 
     def _task_info_path(self, name: str) -> str:
-        return join_paths(self._task_path(name), TASK_INFO_PATH_NAME)
+        return self._task_paths(name)[1]
 
     def _task_status_path(self, name: str) -> str:
-        return join_paths(self._task_path(name), TASK_STATUS_PATH_NAME)
+        return self._task_paths(name)[2]
 
     def _goal_override_path(self, name: str) -> str:
-        return join_paths(self._task_path(name), TASK_METADATA_PATH_NAME, TASK_GOAL_OVERRIDE_PATH_NAME)
+        return self._task_paths(name)[3]
 
     def _goal_override_status_path(self, name: str) -> str:
-        return join_paths(self._task_path(name), TASK_METADATA_PATH_NAME, TASK_GOAL_OVERRIDE_STATUS_PATH_NAME)
+        return self._task_paths(name)[4]
 
     def _property_path(self, key: str) -> str:
         return join_paths(get_service_namespaced_root_path(self.namespace, PROPERTIES_ROOT_NAME), key)
@@ -140,8 +155,7 @@ class StateStore:
 
     def fetch_task_names(self) -> List[str]:
         try:
-            return list(self.persister.get_children(
-                get_service_namespaced_root_path(self.namespace, TASKS_ROOT_NAME)))
+            return list(self.persister.get_children(self._tasks_root))
         except PersisterException as e:
             if e.reason == Reason.NOT_FOUND:
                 return []

@@ -12,6 +12,7 @@ from dcos_commons_amd.scheduler.plan.strategy import (
     DependencyStrategy,
     DependencyStrategyHelper,
     ParallelStrategy,
+    RandomStrategy,
     SerialStrategy,
     phase_strategy_generator,
 )
@@ -199,3 +200,71 @@ def test_coordinator_excludes_dirty_assets():
     assert names(coord.get_candidates()) == ["a-deploy"]
     a1.set_status(S.COMPLETE)
     assert names(coord.get_candidates()) == ["a-other"]
+
+
+# -- cached aggregate statuses (elements._status_gen) --------------------------------------------
+
+def _plan(strategy=SerialStrategy, n=3):
+    steps = [TStep(f"s{i}") for i in range(n)]
+    phase = DefaultPhase("p", steps, strategy())
+    return DefaultPlan("deploy", [phase], SerialStrategy()), phase, steps
+
+
+def test_cached_plan_status_follows_every_kind_of_change():
+    from dcos_commons_amd.scheduler.plan import elements
+
+    plan, phase, steps = _plan()
+    assert plan.get_status() == S.PENDING
+    gen = elements.status_generation()
+    assert plan.get_status() == S.PENDING and plan._status_cache == (gen, S.PENDING)   # served from cache
+    steps[0].set_status(S.COMPLETE)
+    assert phase.get_status() == S.IN_PROGRESS and plan.get_status() == S.IN_PROGRESS
+    phase.interrupt()                                        # strategy flag
+    assert plan.get_status() == S.WAITING
+    phase.proceed()
+    steps[1].interrupt()                                     # step flag: an interrupted PENDING step is WAITING
+    assert steps[1].get_status() == S.WAITING and phase.get_status() == S.WAITING
+    steps[1].proceed()
+    for s in steps:
+        s.force_complete()
+    assert plan.get_status() == S.COMPLETE
+    steps[2].restart()
+    assert plan.get_status() == S.IN_PROGRESS
+
+
+def test_uncacheable_aggregates_are_recomputed():
+    class Flip:                                             # not an AbstractStep: changes unannounced
+        def __init__(self):
+            self.status = S.PENDING
+
+        def get_status(self):
+            return self.status
+
+        def get_errors(self):
+            return []
+
+        def is_interrupted(self):
+            return False
+
+        def get_pod_instance_requirement(self):
+            return None
+
+    f = Flip()
+    phase = DefaultPhase("p", [f], ParallelStrategy())
+    assert phase.get_status() == S.PENDING and phase._status_cache is None
+    f.status = S.COMPLETE
+    assert phase.get_status() == S.COMPLETE
+    plan, phase2, steps = _plan(RandomStrategy)              # random candidates: never cached
+    plan.get_status()
+    assert phase2._status_cache is None and plan._status_cache is None
+
+
+def test_delayed_step_is_not_cached_past_its_backoff():
+    from dcos_commons_amd.scheduler.plan import elements
+
+    plan, phase, steps = _plan(ParallelStrategy, n=1)
+    steps[0].set_status(S.DELAYED)
+    assert phase.get_status() == S.DELAYED
+    assert phase._status_cache is None and not phase._last_cacheable and plan._status_cache is None
+    steps[0]._status = S.PENDING                             # what the backoff expiry does, with no bump
+    assert phase.get_status() == S.PENDING and elements.status_generation() >= 0
