@@ -147,10 +147,14 @@ class OfferEvaluator:
         override_map = {ts.name: self.state_store.fetch_goal_override_status(f"{pi.name}-{ts.name}").target
                         for ts in pi.pod.tasks}
         target_config = self.get_target_config(requirement, this_pod)
+        prototype = None
         for i, offer in enumerate(offers):
             pool = MesosResourcePool(offer, role)
-            builder = PodInfoBuilder(requirement, self.service_name, target_config, self.template_url_factory,
-                                     self.scheduler_config, this_pod.values(), fid_proto, override_map)
+            # one offer-independent build per requirement; each offer's stages work on a copy
+            if prototype is None:
+                prototype = PodInfoBuilder(requirement, self.service_name, target_config, self.template_url_factory,
+                                           self.scheduler_config, this_pod.values(), fid_proto, override_map)
+            builder = prototype.clone() if i + 1 < len(offers) else prototype
             outcomes = []
             failed = 0
             for stage in stages:

@@ -20,7 +20,7 @@ that exist and is never labelled: a lost ACCEPT there is a transient LOST relaun
 from __future__ import annotations
 
 import logging
-from typing import Optional
+from typing import Dict, Optional
 
 from dcos_commons_amd.mesos import protos as P
 from dcos_commons_amd.offer import task_utils
@@ -48,6 +48,14 @@ class PersistentLaunchRecorder:
             pi = self._pod_instance(info)
             if pi is not None and pi.name not in prior_ids:
                 prior_ids[pi.name] = self._stored_resource_ids(pi)
+        # the batch is applied to working copies in recommendation order, then written at once:
+        # TaskInfos in one ``store_tasks`` (the StateStore splits it at 1 MB), statuses after them.
+        # A peer sharing a resource set is rewritten once with the last resources of the batch
+        # instead of once per launched task (a cassandra node: 13 tasks on one set), and only if
+        # they changed.
+        working: Dict[str, P.TaskInfo] = {}
+        fetched: Dict[str, Optional[P.TaskInfo]] = {}
+        statuses = []
         for info in infos:
             status = None
             pi = self._pod_instance(info)
@@ -60,10 +68,15 @@ class PersistentLaunchRecorder:
                 new = bool(ids) and pi is not None and not (set(ids) & prior_ids.get(pi.name, set()))
                 TaskLabelWriter(info).set_launch_new_footprint(new).apply()
             if pi is not None:
-                self._update_resource_set_peers(pi, info)
-            self.state_store.store_tasks([info])
+                self._update_resource_set_peers(pi, info, working, fetched)
+            working.pop(info.name, None)
+            working[info.name] = info
             if status is not None:
-                self.state_store.store_status(info.name, status)
+                statuses.append((info.name, status))
+        if working:
+            self.state_store.store_tasks(list(working.values()))
+        for name, status in statuses:
+            self.state_store.store_status(name, status)
 
     def _pod_instance(self, info: P.TaskInfo) -> Optional[PodInstance]:
         try:
@@ -80,26 +93,42 @@ class PersistentLaunchRecorder:
                 out.update(get_resource_ids(get_all_resources(stored)))
         return out
 
-    def _update_resource_set_peers(self, pi: PodInstance, info: P.TaskInfo) -> None:
+    def _update_resource_set_peers(self, pi: PodInstance, info: P.TaskInfo,
+                                   working: Optional[Dict[str, P.TaskInfo]] = None,
+                                   fetched: Optional[Dict[str, Optional[P.TaskInfo]]] = None) -> None:
+        """Copies ``info``'s task and executor resources onto the other tasks of its resource set
+        (PersistentLaunchRecorder.updateResourcesWithinResourceSet): into ``working`` during a
+        batch, or straight to the StateStore without one. ``fetched`` memoizes the stored peers
+        read during the batch, so a set of N tasks is read N times, not N squared."""
         spec = task_utils.get_task_spec(pi, info.name)
         if spec is None:
             return
-        peers = []
+        standalone = working is None
+        if standalone:
+            working = {}
+        if fetched is None:
+            fetched = {}
+        has_executor = info.HasField("executor")
         for t in pi.pod.tasks:
             if t.name == spec.name or t.resource_set != spec.resource_set:
                 continue
-            peer = self.state_store.fetch_task(f"{pi.name}-{t.name}")
-            if peer is not None:
-                peers.append(peer)
-        updated = []
-        for peer in peers:
-            c = P.TaskInfo()
-            c.CopyFrom(peer)
-            del c.resources[:]
-            c.resources.extend(info.resources)
-            if info.HasField("executor"):
-                del c.executor.resources[:]
-                c.executor.resources.extend(info.executor.resources)
-            updated.append(c)
-        if updated:
-            self.state_store.store_tasks(updated)
+            name = f"{pi.name}-{t.name}"
+            peer = working.get(name)
+            if peer is None:
+                if name not in fetched:
+                    fetched[name] = self.state_store.fetch_task(name)
+                stored = fetched[name]
+                if stored is None:
+                    continue
+                if list(stored.resources) == list(info.resources) and (
+                        not has_executor or list(stored.executor.resources) == list(info.executor.resources)):
+                    continue  # already what this launch would write
+                peer = stored
+            del peer.resources[:]
+            peer.resources.extend(info.resources)
+            if has_executor:
+                del peer.executor.resources[:]
+                peer.executor.resources.extend(info.executor.resources)
+            working[name] = peer
+        if standalone and working:
+            self.state_store.store_tasks(list(working.values()))

@@ -628,3 +628,22 @@ def test_task_without_tls_passes_untouched():
     updater = RecordingUpdater()
     b = _launch_builder()
     assert _tls_stage(updater).evaluate(_pool(U.get_offer()), b).passing and updater.calls == []
+
+
+def test_pod_info_builder_clone_is_an_independent_fresh_build():
+    pod = _pod_spec(_task_yaml(ports="""\
+        http:
+          port: 0
+    """))
+    proto = _builder(pod)
+    fresh = _builder(pod)
+    a, b = proto.clone(), proto.clone()
+    a.get_task_builder(TASK).command.value = "changed"
+    a.add_assigned_overlay_port(1234)
+    a.get_executor_builder().executor_id.value = "exec"
+    assert b.get_task_builder(TASK).command.value == fresh.get_task_builder(TASK).command.value == "./cmd"
+    assert not b.is_assigned_overlay_port(1234) and not proto.is_assigned_overlay_port(1234)
+    assert proto.get_executor_builder().executor_id.value == ""
+    # labels other than the target configuration (random per build here) match a fresh build
+    assert b.get_task_builder(TASK).name == fresh.get_task_builder(TASK).name
+    assert b.get_task_builder(TASK).container == fresh.get_task_builder(TASK).container

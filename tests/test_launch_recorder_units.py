@@ -170,3 +170,81 @@ def test_schema_version_store_rejects_unknown_and_reports_write_failures():
         SchemaVersionStore(MemPersister()).store(SchemaVersion.UNKNOWN)
     with pytest.raises(StateStoreException):
         SchemaVersionStore(BrokenPersister()).store(SchemaVersion.MULTI_SERVICE)
+
+
+# ---------------------------------------------------------------------------------------
+# batched recording: the final state of the reference's write-per-task sequence, written once
+
+
+class CountingPersister(MemPersister):
+    def __init__(self):
+        super().__init__()
+        self.writes = []
+
+    def set(self, path, value):
+        self.writes.append(path)
+        super().set(path, value)
+
+    def set_many(self, mapping):
+        self.writes.extend(mapping)
+        super().set_many(mapping)
+
+
+def _sequential_record(store, recorder, recs):
+    """The reference's order (PersistentLaunchRecorder.record): each TaskInfo stored with its
+    resource-set peers rewritten from the store, then its STAGING status."""
+    stores = sorted((r for r in recs if isinstance(r, StoreTaskInfoRecommendation)),
+                    key=lambda r: len(r.task_info.task_id.value))
+    for rec in stores:
+        info = rec.state_store_task_info()
+        pi = recorder._pod_instance(info)
+        if pi is not None:
+            recorder._update_resource_set_peers(pi, info)
+        store.store_tasks([info])
+        if info.task_id.value:
+            st = P.TaskStatus(state=P.TASK_STAGING)
+            st.task_id.CopyFrom(info.task_id)
+            store.store_status(info.name, st)
+
+
+def test_batched_record_matches_the_sequential_final_state():
+    new_res = [_cpus(3.0)]
+    recs = [_store(_task("pod-0-server", "pod", 0, new_res, task_id=P.TaskID(value="pod-0-server__new"))),
+            _store(_task("pod-0-init", "pod", 0, new_res, task_id=P.TaskID(value="")))]
+    finals = []
+    for batched in (True, False):
+        store = StateStore(MemPersister())
+        recorder = PersistentLaunchRecorder(store, SPEC)
+        store.store_tasks([_task("pod-0-init", "pod", 0, [_cpus(1.0)]), _task("pod-1-init", "pod", 1, [_cpus(2.0)])])
+        if batched:
+            recorder.record(recs)
+        else:
+            _sequential_record(store, recorder, recs)
+        finals.append({n: (store.fetch_task(n).SerializeToString(deterministic=True),
+                           store.fetch_status(n) and store.fetch_status(n).state)
+                       for n in store.fetch_task_names()})
+    # the launch-footprint label is the batched recorder's own addition: compare without it
+    for f in finals:
+        for n, (data, st) in list(f.items()):
+            t = P.TaskInfo()
+            t.ParseFromString(data)
+            for label in list(t.labels.labels):
+                if label.key == "launch_new_footprint":
+                    t.labels.labels.remove(label)
+            f[n] = (t.SerializeToString(deterministic=True), st)
+    assert finals[0] == finals[1]
+    assert finals[0]["pod-1-init"][0] == _task("pod-1-init", "pod", 1, [_cpus(2.0)]).SerializeToString(
+        deterministic=True)
+
+
+def test_record_writes_each_task_once_and_skips_unchanged_peers():
+    p = CountingPersister()
+    store = StateStore(p)
+    recorder = PersistentLaunchRecorder(store, SPEC)
+    same = [_cpus(1.0)]
+    store.store_tasks([_task("pod-0-init", "pod", 0, same)])
+    p.writes.clear()
+    recorder.record([_store(_task("pod-0-server", "pod", 0, same, task_id=P.TaskID(value="pod-0-server__x")))])
+    task_writes = [w for w in p.writes if w.endswith("/TaskInfo")]
+    assert task_writes == ["Tasks/pod-0-server/TaskInfo"]  # the peer already holds these resources
+    assert store.fetch_status("pod-0-server").state == P.TASK_STAGING
