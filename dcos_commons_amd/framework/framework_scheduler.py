@@ -159,6 +159,7 @@ class FrameworkScheduler:
             reconciling = awaiting is not None and awaiting()
             with trace.span("status", "status", task=status.task_id.value, state=P.TaskState.Name(status.state)):
                 resp = self.client.task_status(status)
+            relaunch_kill = task_killer.ends_relaunch_kill(status)
             eligible = task_killer.update(status)
             if resp.result == TaskStatusResult.UNKNOWN_TASK:
                 if eligible:
@@ -168,8 +169,17 @@ class FrameworkScheduler:
                 else:
                     LOGGER.warning("Received status update for unknown task, but task should not be killed "
                                    "again: %s", status.task_id.value)
-            if resp.result == TaskStatusResult.UNKNOWN_TASK or reconciling or can_create_work(status):
+            # The end of a kill issued for a relaunch frees the killed task's reservations. A
+            # revive has the master offer them now: for an in-place relaunch that offer carries
+            # what the relaunch needs (and wakes the loop for it; a cycle now would re-evaluate
+            # against the offers in hand, which cannot hold them), for a replacement placed
+            # elsewhere it carries the stale reservations to release, which a scheduler that has
+            # gone idle (suppressed) would otherwise never be offered.
+            if resp.result == TaskStatusResult.UNKNOWN_TASK or reconciling or \
+                    (can_create_work(status) and not relaunch_kill):
                 self.offer_processor.kick()
+            if relaunch_kill:
+                self.offer_processor.revive_for_relaunch()
         except Exception as e:  # noqa: BLE001
             self._exit(e)
 

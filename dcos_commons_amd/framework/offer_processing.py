@@ -44,6 +44,11 @@ DEFAULT_QUEUE_CAPACITY = 100
 ACCEPT_FILTERS = P.Filters(refuse_seconds=1)
 
 
+# after a revive-only wake-up (a relaunch kill ended), the longest wait for the re-offer before a
+# full cycle re-evaluates the offers in hand
+RELAUNCH_FALLBACK_CYCLE_S = 0.05
+
+
 class OfferQueue:
     def __init__(self, capacity: int = DEFAULT_QUEUE_CAPACITY):
         self.capacity = capacity
@@ -210,8 +215,10 @@ class ReviveManager:
         if self.is_suppressed:
             self.request_revive()
 
-    def request_revive(self) -> None:
-        if self.is_suppressed and self.fast_unsuppress:
+    def request_revive(self, bypass_spacing: bool = False) -> None:
+        """``bypass_spacing``: a one-off revive for a known event (a pod's reservations freed for
+        its relaunch) that is not held to the burst spacing; it still spends a token."""
+        if bypass_spacing or (self.is_suppressed and self.fast_unsuppress):
             self._revive_bypass = True
         self.revive_requested = True
 
@@ -456,6 +463,13 @@ class OfferProcessor:
         self._in_progress = set()
         self._in_progress_lock = threading.Lock()
         self._wake = threading.Event()
+        # why the loop was woken: ``kick`` asks for a full cycle; ``revive_for_relaunch`` only for
+        # a revive (both are read and reset by the offer thread at the start of a cycle)
+        self._eval_wake = False
+        self._relaunch_revive = False
+        # after a revive-only wake-up, a full cycle runs at this time unless an offer or a kick
+        # brings one sooner (a kill of a task the master did not know frees nothing to re-offer)
+        self._fallback_cycle_at: Optional[float] = None
         self._stop = threading.Event()
         self._thread: Optional[threading.Thread] = None
         self.cycles = 0
@@ -489,6 +503,9 @@ class OfferProcessor:
                     # a throttled revive is retried the moment the bucket allows it, not at the
                     # next offer poll
                     wait = min(wait, max(0.001, self.revive_manager.bucket.seconds_until_available()))
+                fallback = self._fallback_cycle_at
+                if fallback is not None:
+                    wait = min(wait, max(0.0, fallback - time.monotonic()))
                 self.process_queued_offers(wait)
             except Exception as e:  # noqa: BLE001
                 LOGGER.exception("Error encountered when processing offers, exiting to avoid zombie state")
@@ -498,6 +515,18 @@ class OfferProcessor:
     def kick(self) -> None:
         """Wake the loop now (status update / plan change) instead of at the next offer poll."""
         if self.event_driven:
+            self._eval_wake = True
+            self._wake.set()
+            self.queue.notify()
+
+    def revive_for_relaunch(self) -> None:
+        """A kill issued to relaunch a pod in place has ended: the pod's reservations are free at
+        the master, which offers them again at its next allocation. Wake the loop for a REVIVE
+        (allocation now) instead of a cycle: the offers in hand cannot hold those reservations,
+        and the offer that carries them wakes the loop for the relaunch. The revive is taken on
+        the offer thread, like every revive (OfferProcessor.java:300-309)."""
+        if self.event_driven:
+            self._relaunch_revive = True
             self._wake.set()
             self.queue.notify()
 
@@ -541,6 +570,14 @@ class OfferProcessor:
         new_offers = self.queue.take_all(wait_s, self._wake if self.event_driven else None)
         if self._stop.is_set():
             return
+        relaunch_revive, self._relaunch_revive = self._relaunch_revive, False
+        eval_wake, self._eval_wake = self._eval_wake, False
+        if relaunch_revive and not new_offers and not eval_wake:
+            self.revive_manager.request_revive(bypass_spacing=True)
+            self.revive_manager.revive_if_requested()
+            self._fallback_cycle_at = time.monotonic() + RELAUNCH_FALLBACK_CYCLE_S
+            return
+        self._fallback_cycle_at = None
         now = time.monotonic()
         with self._held_lock:
             held = [o for o, _ in self._held.values()]
@@ -567,6 +604,7 @@ class OfferProcessor:
                             self.client.consume_recheck_request():
                         # the client started work that changes its status (e.g. uninstall's
                         # deregister step): re-check now rather than at the next offer poll
+                        self._eval_wake = True
                         self._wake.set()
                 elif self._deregistered:
                     # the framework was just torn down: its offers went with it
@@ -579,6 +617,10 @@ class OfferProcessor:
                     if self.gc_all_offers:
                         offers = self._collect_garbage(offers)
                     decline_long(offers)
+            if relaunch_revive:
+                # requested after the cycle's own revive bookkeeping, so neither a suppress nor
+                # a cancelled work-set revive drops it
+                self.revive_manager.request_revive(bypass_spacing=True)
             self.revive_manager.revive_if_requested()
         finally:
             metrics.increment_processed_offers(len(new_offers))

@@ -20,6 +20,9 @@ KILL_INTERVAL_S = 5.0
 
 _lock = new_lock("TaskKiller")
 _tasks_to_kill: Set[str] = set()
+# kills the plan scheduler issued to relaunch a pod in place: their terminal status frees
+# reservations that come back in a new offer, so the status itself gives the offer loop nothing to do
+_relaunch_kills: Set[str] = set()
 _thread = None
 _stop_event = threading.Event()
 _executor_enabled = True
@@ -37,6 +40,7 @@ def reset(executor_enabled: bool = True) -> None:
             t = None
         _thread = None
         _tasks_to_kill.clear()
+        _relaunch_kills.clear()
         _executor_enabled = executor_enabled
     if t is not None:
         t.join(timeout=KILL_INTERVAL_S)
@@ -48,13 +52,17 @@ def _loop() -> None:
         kill_all_tasks()
 
 
-def kill_task(task_id: P.TaskID) -> None:
+def kill_task(task_id: P.TaskID, relaunch: bool = False) -> None:
+    """``relaunch``: the kill frees the task's resources for a relaunch of its pod that the plan
+    scheduler is already evaluating (PlanScheduler.killTasks)."""
     global _thread
     if not task_id.value:
         LOGGER.warning("Attempted to kill empty TaskID.")
         return
     with _lock:
         _tasks_to_kill.add(task_id.value)
+        if relaunch:
+            _relaunch_kills.add(task_id.value)
         if _thread is None and _executor_enabled:
             _thread = threading.Thread(target=_loop, name="TaskKiller", daemon=True)
             _thread.start()
@@ -66,10 +74,19 @@ def update(status: P.TaskStatus) -> bool:
     if status.state in _ALIVE:
         return True
     with _lock:
+        _relaunch_kills.discard(status.task_id.value)
         if status.task_id.value in _tasks_to_kill:
             _tasks_to_kill.discard(status.task_id.value)
             return False
     return True
+
+
+def ends_relaunch_kill(status: P.TaskStatus) -> bool:
+    """Whether ``status`` is the terminal status of a relaunch kill (call before ``update``)."""
+    if status.state in _ALIVE:
+        return False
+    with _lock:
+        return status.task_id.value in _relaunch_kills
 
 
 def pending_kills() -> Set[str]:

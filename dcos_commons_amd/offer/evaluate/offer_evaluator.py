@@ -195,17 +195,25 @@ class OfferEvaluator:
                         s.add_failure_reason(o.source)
 
     # -- pipelines ---------------------------------------------------------------------
-    def get_evaluation_pipeline(self, requirement: PodInstanceRequirement, all_tasks, this_pod: Dict[str, P.TaskInfo]):
+    @staticmethod
+    def _uses_new_pipeline(requirement: PodInstanceRequirement, this_pod: Dict[str, P.TaskInfo]) -> bool:
+        """New footprint (OfferEvaluator.java:250-262): a permanent replace, a pod whose tasks are
+        all permanently failed, or one that never reserved anything; otherwise an in-place relaunch
+        on the pod's existing reservations."""
         ids = [get_resource_id(r) for t in this_pod.values() for r in t.resources]
         no_launched = all((i or "") == "" for i in ids if i is not None)
         all_perm_failed = bool(this_pod) and all(TaskLabelReader(t).is_permanently_failed()
                                                  for t in this_pod.values())
-        if requirement.recovery_type == RecoveryType.PERMANENT or all_perm_failed:
-            new = True
-        elif no_launched:
-            new = True
-        else:
-            new = False
+        return requirement.recovery_type == RecoveryType.PERMANENT or all_perm_failed or no_launched
+
+    def relaunches_in_place(self, requirement: PodInstanceRequirement, all_tasks: Dict[str, P.TaskInfo]) -> bool:
+        """Whether ``requirement`` is evaluated with the existing pipeline: it needs the pod's
+        own reservations, which no offer carries while a task of the pod still runs on them."""
+        this_pod = {n: all_tasks[n] for n in task_utils.get_task_names(requirement.pod_instance) if n in all_tasks}
+        return bool(this_pod) and not self._uses_new_pipeline(requirement, this_pod)
+
+    def get_evaluation_pipeline(self, requirement: PodInstanceRequirement, all_tasks, this_pod: Dict[str, P.TaskInfo]):
+        new = self._uses_new_pipeline(requirement, this_pod)
         pod = requirement.pod_instance.pod
         tls = self.tls_stage_factory if any(t.transport_encryption for t in pod.tasks) else None
         if new:

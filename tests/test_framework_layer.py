@@ -614,3 +614,94 @@ def test_cpu_set_flag():
             parse_cpu_list(bad)
     assert SchedulerConfig.for_testing().cpu_set() is None
     assert SchedulerConfig.for_testing(SDK_CPU_SET="2,3").cpu_set() == [2, 3]
+
+
+# ---------------------------------------------------------------------------------------
+# relaunch kills: their end asks for a revive, not an offer cycle
+
+
+def _status(tid, state):
+    s = P.TaskStatus(state=state)
+    s.task_id.value = tid
+    return s
+
+
+def test_task_killer_tracks_relaunch_kills(drv):
+    task_killer.kill_task(P.TaskID(value="relaunched"), relaunch=True)
+    task_killer.kill_task(P.TaskID(value="plain"))
+    assert drv.kills == ["relaunched", "plain"]
+    assert not task_killer.ends_relaunch_kill(_status("relaunched", P.TASK_KILLING))   # not terminal yet
+    assert task_killer.ends_relaunch_kill(_status("relaunched", P.TASK_KILLED))
+    assert not task_killer.ends_relaunch_kill(_status("plain", P.TASK_KILLED))
+    assert task_killer.update(_status("relaunched", P.TASK_KILLED)) is False          # expected death
+    assert not task_killer.ends_relaunch_kill(_status("relaunched", P.TASK_KILLED))   # consumed
+
+
+class CountingClient(Client):
+    def __init__(self, **kw):
+        super().__init__(**kw)
+        self.status_calls = 0
+
+    def get_client_status(self):
+        self.status_calls += 1
+        return super().get_client_status()
+
+
+def test_relaunch_revive_wakes_for_a_revive_only(drv):
+    c = CountingClient()
+    from dcos_commons_amd.framework.offer_processing import TokenBucket
+
+    p = processor(c, hold_s=10.0, event_driven=True,
+                  token_bucket=TokenBucket(acquire_interval_s=5.0, burst_interval_s=1.0)).disable_threading()
+    p.start()   # no thread: the cycles are driven below
+    p.revive_manager.bucket.try_acquire()     # a revive just happened: the burst spacing is running
+    p.revive_for_relaunch()
+    p.process_queued_offers(0.5)
+    # one revive, despite the spacing (it spends a token), and no client status / evaluation pass
+    assert drv.revives == 1 and c.status_calls == 0 and not p.revive_manager.revive_requested
+    # a kick in the same wake-up asks for a full cycle as well
+    p.revive_for_relaunch()
+    p.kick()
+    p.process_queued_offers(0.5)
+    assert c.status_calls == 1 and drv.revives == 2
+    # without event-driven wake-ups (the reference cadence) nothing is requested
+    q = processor(CountingClient())
+    q.revive_for_relaunch()
+    assert not q._relaunch_revive
+
+
+def test_relaunch_kill_status_revives_instead_of_kicking(drv):
+    from dcos_commons_amd.framework.framework_scheduler import FrameworkScheduler
+    from dcos_commons_amd.scheduler.mesos_event_client import TaskStatusResponse
+
+    calls = []
+
+    class OP:
+        def kick(self):
+            calls.append("kick")
+
+        def revive_for_relaunch(self):
+            calls.append("revive")
+
+    class C:
+        def task_status(self, status):
+            return TaskStatusResponse.processed()
+
+    class Unknown:
+        def task_status(self, status):
+            return TaskStatusResponse.unknown_task()
+
+    fs = FrameworkScheduler.__new__(FrameworkScheduler)
+    fs.client, fs.offer_processor = C(), OP()
+    task_killer.kill_task(P.TaskID(value="t1"), relaunch=True)
+    fs.status_update(drv, _status("t1", P.TASK_KILLED))
+    task_killer.kill_task(P.TaskID(value="t2"))
+    fs.status_update(drv, _status("t2", P.TASK_KILLED))
+    assert calls == ["revive", "kick"]
+    # a replaced task's end arrives after its successor was stored (unknown task): a full cycle,
+    # and a revive so the master offers the stale reservations for release even if we are idle
+    calls.clear()
+    fs.client = Unknown()
+    task_killer.kill_task(P.TaskID(value="t3"), relaunch=True)
+    fs.status_update(drv, _status("t3", P.TASK_KILLED))
+    assert calls == ["kick", "revive"]
