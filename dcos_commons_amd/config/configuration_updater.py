@@ -108,6 +108,8 @@ class DefaultConfigurationUpdater:
         return replace(target, user=target.user or DEFAULT_SERVICE_USER, pods=pods)
 
     def _print_diff(self, old, old_id, new) -> None:
+        if not self.logger.isEnabledFor(logging.INFO):
+            return  # the diff of two rendered specs is the costliest part of a restart's update
         try:
             diff = difflib.unified_diff(old.to_json_string().splitlines(), new.to_json_string().splitlines(),
                                         "ServiceSpec.old", "ServiceSpec.new", n=2, lineterm="")

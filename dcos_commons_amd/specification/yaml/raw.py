@@ -19,7 +19,9 @@ class RawSpecError(ValueError):
     pass
 
 
-class _StrictLoader(yaml.SafeLoader):
+# libyaml's scanner/parser when PyYAML was built with it (same YAML 1.1 grammar and safe
+# constructors; ~4x faster on a 600-line svc.yml, which every scheduler start parses)
+class _StrictLoader(getattr(yaml, "CSafeLoader", yaml.SafeLoader)):
     pass
 
 
