@@ -169,17 +169,19 @@ class FrameworkScheduler:
                 else:
                     LOGGER.warning("Received status update for unknown task, but task should not be killed "
                                    "again: %s", status.task_id.value)
-            # The end of a kill issued for a relaunch frees the killed task's reservations. A
-            # revive has the master offer them now: for an in-place relaunch that offer carries
-            # what the relaunch needs (and wakes the loop for it; a cycle now would re-evaluate
-            # against the offers in hand, which cannot hold them), for a replacement placed
-            # elsewhere it carries the stale reservations to release, which a scheduler that has
-            # gone idle (suppressed) would otherwise never be offered.
+            # A task that ended after a kill issued for a relaunch, or a FINISH/ONCE task that
+            # finished, released reservations the plans reuse. A revive has the master offer them
+            # now: for an in-place relaunch (or the pod's next step) that offer carries what it
+            # needs, and wakes the loop for it (a cycle now would re-evaluate against the offers
+            # in hand, which cannot hold them); for a replacement placed elsewhere it carries the
+            # stale reservations to release, which a scheduler that has gone idle (suppressed)
+            # would otherwise never be offered.
+            finished = status.state == P.TASK_FINISHED and resp.result != TaskStatusResult.UNKNOWN_TASK
             if resp.result == TaskStatusResult.UNKNOWN_TASK or reconciling or \
                     (can_create_work(status) and not relaunch_kill):
                 self.offer_processor.kick()
-            if relaunch_kill:
-                self.offer_processor.revive_for_relaunch()
+            if relaunch_kill or finished:
+                self.offer_processor.reoffer_released()
         except Exception as e:  # noqa: BLE001
             self._exit(e)
 

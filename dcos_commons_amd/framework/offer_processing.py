@@ -46,7 +46,7 @@ ACCEPT_FILTERS = P.Filters(refuse_seconds=1)
 
 # after a revive-only wake-up (a relaunch kill ended), the longest wait for the re-offer before a
 # full cycle re-evaluates the offers in hand
-RELAUNCH_FALLBACK_CYCLE_S = 0.05
+REOFFER_FALLBACK_CYCLE_S = 0.05
 
 
 class OfferQueue:
@@ -216,9 +216,12 @@ class ReviveManager:
             self.request_revive()
 
     def request_revive(self, bypass_spacing: bool = False) -> None:
-        """``bypass_spacing``: a one-off revive for a known event (a pod's reservations freed for
-        its relaunch) that is not held to the burst spacing; it still spends a token."""
-        if bypass_spacing or (self.is_suppressed and self.fast_unsuppress):
+        """``bypass_spacing``: a one-off revive for a known event (reservations released for a
+        relaunch) that is not held to the burst spacing while the bucket is above its burst floor;
+        it still spends a token, and a drained bucket (a crash loop) keeps the slow spacing."""
+        if bypass_spacing and self.bucket.count > self.bucket.burst_floor:
+            self._revive_bypass = True
+        if self.is_suppressed and self.fast_unsuppress:
             self._revive_bypass = True
         self.revive_requested = True
 
@@ -463,10 +466,10 @@ class OfferProcessor:
         self._in_progress = set()
         self._in_progress_lock = threading.Lock()
         self._wake = threading.Event()
-        # why the loop was woken: ``kick`` asks for a full cycle; ``revive_for_relaunch`` only for
-        # a revive (both are read and reset by the offer thread at the start of a cycle)
+        # why the loop was woken: ``kick`` asks for a full cycle; ``reoffer_released`` for a revive
+        # (both are read and reset by the offer thread at the start of a cycle)
         self._eval_wake = False
-        self._relaunch_revive = False
+        self._reoffer = False
         # after a revive-only wake-up, a full cycle runs at this time unless an offer or a kick
         # brings one sooner (a kill of a task the master did not know frees nothing to re-offer)
         self._fallback_cycle_at: Optional[float] = None
@@ -519,14 +522,15 @@ class OfferProcessor:
             self._wake.set()
             self.queue.notify()
 
-    def revive_for_relaunch(self) -> None:
-        """A kill issued to relaunch a pod in place has ended: the pod's reservations are free at
-        the master, which offers them again at its next allocation. Wake the loop for a REVIVE
-        (allocation now) instead of a cycle: the offers in hand cannot hold those reservations,
-        and the offer that carries them wakes the loop for the relaunch. The revive is taken on
+    def reoffer_released(self) -> None:
+        """A task ended that held reservations the plans reuse in place: a kill issued for a
+        relaunch, or a FINISH/ONCE task whose pod's next step runs on the same resource set. The
+        master offers released resources again at its next allocation; wake the loop for a REVIVE
+        (an allocation now) that is not held to the burst spacing while the bucket is above its
+        floor. The offer that carries them wakes the loop for the relaunch. The revive is taken on
         the offer thread, like every revive (OfferProcessor.java:300-309)."""
         if self.event_driven:
-            self._relaunch_revive = True
+            self._reoffer = True
             self._wake.set()
             self.queue.notify()
 
@@ -570,12 +574,12 @@ class OfferProcessor:
         new_offers = self.queue.take_all(wait_s, self._wake if self.event_driven else None)
         if self._stop.is_set():
             return
-        relaunch_revive, self._relaunch_revive = self._relaunch_revive, False
+        reoffer, self._reoffer = self._reoffer, False
         eval_wake, self._eval_wake = self._eval_wake, False
-        if relaunch_revive and not new_offers and not eval_wake:
+        if reoffer and not new_offers and not eval_wake:
             self.revive_manager.request_revive(bypass_spacing=True)
             self.revive_manager.revive_if_requested()
-            self._fallback_cycle_at = time.monotonic() + RELAUNCH_FALLBACK_CYCLE_S
+            self._fallback_cycle_at = time.monotonic() + REOFFER_FALLBACK_CYCLE_S
             return
         self._fallback_cycle_at = None
         now = time.monotonic()
@@ -617,7 +621,7 @@ class OfferProcessor:
                     if self.gc_all_offers:
                         offers = self._collect_garbage(offers)
                     decline_long(offers)
-            if relaunch_revive:
+            if reoffer:
                 # requested after the cycle's own revive bookkeeping, so neither a suppress nor
                 # a cancelled work-set revive drops it
                 self.revive_manager.request_revive(bypass_spacing=True)

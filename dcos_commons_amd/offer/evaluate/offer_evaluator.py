@@ -26,6 +26,7 @@ from dcos_commons_amd.scheduler.plan.pod_instance_requirement import PodInstance
 from dcos_commons_amd.specification.specs import GoalState, NamedVIPSpec, PortSpec, ResourceSpec
 from dcos_commons_amd.utils.logging_utils import get_logger
 
+from .outcome import EvaluationOutcome
 from .pod_info_builder import PodInfoBuilder
 from .resource_mappers import ExecutorResourceMapper, TaskResourceMapper
 from .stages import (
@@ -68,6 +69,13 @@ def _outcome_reasons(out: List[str], outcome) -> None:
     out.append(f"{'PASS' if outcome.passing else 'FAIL'}({outcome.source}):{outcome.reason}")
     for c in outcome.children:
         _outcome_reasons(out, c)
+
+
+def _required_reservations(stages) -> set:
+    """Reservation IDs the pipeline's task resource and volume stages consume by ID (executor
+    resources are left out: a running executor's are not taken from the offer)."""
+    return {s.resource_id for s in stages
+            if isinstance(s, (ResourceEvaluationStage, VolumeEvaluationStage)) and s.task_names and s.resource_id}
 
 
 class _LazyText:
@@ -147,8 +155,22 @@ class OfferEvaluator:
         override_map = {ts.name: self.state_store.fetch_goal_override_status(f"{pi.name}-{ts.name}").target
                         for ts in pi.pod.tasks}
         target_config = self.get_target_config(requirement, this_pod)
+        required = _required_reservations(stages)
         prototype = None
         for i, offer in enumerate(offers):
+            if required:
+                missing = required.difference(get_resource_id(r) for r in offer.resources)
+                if missing:
+                    # an in-place relaunch consumes these reservations by ID: an offer without
+                    # one of them fails its resource/volume stage whatever else it holds (e.g. an
+                    # offer from another agent, or from the pod's agent while a killed task still
+                    # holds them), so the pipeline is not run on it
+                    o = EvaluationOutcome.fail(
+                        "ReservationPrecheck", "Offer lacks %d of the %d reservation(s) this relaunch reuses: %s",
+                        len(missing), len(required), sorted(missing))
+                    self.logger.info("Offer %d, %s: %s for %s", i + 1, offer.id.value, o.reason, requirement.name)
+                    self._track(requirement, False, offer, lambda o=o: "\n".join(_outcome_lines(o)), [o])
+                    continue
             pool = MesosResourcePool(offer, role)
             # one offer-independent build per requirement; each offer's stages work on a copy
             if prototype is None:
@@ -205,12 +227,6 @@ class OfferEvaluator:
         all_perm_failed = bool(this_pod) and all(TaskLabelReader(t).is_permanently_failed()
                                                  for t in this_pod.values())
         return requirement.recovery_type == RecoveryType.PERMANENT or all_perm_failed or no_launched
-
-    def relaunches_in_place(self, requirement: PodInstanceRequirement, all_tasks: Dict[str, P.TaskInfo]) -> bool:
-        """Whether ``requirement`` is evaluated with the existing pipeline: it needs the pod's
-        own reservations, which no offer carries while a task of the pod still runs on them."""
-        this_pod = {n: all_tasks[n] for n in task_utils.get_task_names(requirement.pod_instance) if n in all_tasks}
-        return bool(this_pod) and not self._uses_new_pipeline(requirement, this_pod)
 
     def get_evaluation_pipeline(self, requirement: PodInstanceRequirement, all_tasks, this_pod: Dict[str, P.TaskInfo]):
         new = self._uses_new_pipeline(requirement, this_pod)

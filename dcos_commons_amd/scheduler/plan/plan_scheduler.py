@@ -18,17 +18,10 @@ from typing import List, Optional
 
 from dcos_commons_amd.framework import task_killer
 from dcos_commons_amd.offer.recommendations import StoreTaskInfoRecommendation
-from dcos_commons_amd.offer.resources import get_all_resources, get_resource_id, get_resource_ids
 from dcos_commons_amd.offer.task_utils import is_terminal
 from dcos_commons_amd.utils.logging_utils import get_logger
 
 LOGGER = logging.getLogger(__name__)
-
-
-def _offers_carry(offers, killed) -> bool:
-    """Whether any offer holds a reservation of a killed task."""
-    ids = set().union(*killed)
-    return any(get_resource_id(r) in ids for o in offers for r in o.resources)
 
 
 class PlanScheduler:
@@ -66,16 +59,7 @@ class PlanScheduler:
         if req is None:
             step.update_offer_status([])
             return []
-        killed = self._kill_tasks(req)
-        if killed and not _offers_carry(offers, killed) and self.offer_evaluator.relaunches_in_place(req, all_tasks):
-            # the relaunch reuses the reservations of the tasks just killed and no offer in hand
-            # carries any of them (a master does not offer reservations a live task holds), so
-            # evaluating now can only fail (the reference evaluates anyway). The kills' terminal
-            # statuses bring them back (a revive, then the master's offer).
-            self.logger.info("Waiting for %d killed task(s) of %s to release their reservations",
-                             len(killed), step.get_name())
-            step.update_offer_status([])
-            return []
+        self._kill_tasks(req)
         try:
             recs = self.offer_evaluator.evaluate(req, offers, all_tasks)
         except Exception:  # noqa: BLE001
@@ -89,10 +73,9 @@ class PlanScheduler:
         step.update_offer_status([r for r in recs if r.get_operation() is not None])
         return recs
 
-    def _kill_tasks(self, req) -> List[set]:
-        """Kills the live tasks on the resource sets ``req`` relaunches; returns the reservation
-        IDs of each task killed."""
-        killed = []
+    def _kill_tasks(self, req) -> None:
+        """Kills the live tasks on the resource sets ``req`` relaunches (as relaunch kills: their
+        end asks the master to offer the freed reservations again)."""
         pi = req.pod_instance
         sets = {t.resource_set.id for t in pi.pod.tasks if t.name in req.tasks_to_launch}
         for t in pi.pod.tasks:
@@ -105,5 +88,3 @@ class PlanScheduler:
             status = self.state_store.fetch_status(name)
             if status is None or not is_terminal(status):
                 task_killer.kill_task(info.task_id, relaunch=True)
-                killed.append(set(get_resource_ids(get_all_resources(info))))
-        return killed

@@ -647,7 +647,7 @@ class CountingClient(Client):
         return super().get_client_status()
 
 
-def test_relaunch_revive_wakes_for_a_revive_only(drv):
+def test_reoffer_wakes_for_a_revive_only(drv):
     c = CountingClient()
     from dcos_commons_amd.framework.offer_processing import TokenBucket
 
@@ -655,19 +655,19 @@ def test_relaunch_revive_wakes_for_a_revive_only(drv):
                   token_bucket=TokenBucket(acquire_interval_s=5.0, burst_interval_s=1.0)).disable_threading()
     p.start()   # no thread: the cycles are driven below
     p.revive_manager.bucket.try_acquire()     # a revive just happened: the burst spacing is running
-    p.revive_for_relaunch()
+    p.reoffer_released()
     p.process_queued_offers(0.5)
     # one revive, despite the spacing (it spends a token), and no client status / evaluation pass
     assert drv.revives == 1 and c.status_calls == 0 and not p.revive_manager.revive_requested
     # a kick in the same wake-up asks for a full cycle as well
-    p.revive_for_relaunch()
+    p.reoffer_released()
     p.kick()
     p.process_queued_offers(0.5)
     assert c.status_calls == 1 and drv.revives == 2
     # without event-driven wake-ups (the reference cadence) nothing is requested
     q = processor(CountingClient())
-    q.revive_for_relaunch()
-    assert not q._relaunch_revive
+    q.reoffer_released()
+    assert not q._reoffer
 
 
 def test_relaunch_kill_status_revives_instead_of_kicking(drv):
@@ -680,7 +680,7 @@ def test_relaunch_kill_status_revives_instead_of_kicking(drv):
         def kick(self):
             calls.append("kick")
 
-        def revive_for_relaunch(self):
+        def reoffer_released(self):
             calls.append("revive")
 
     class C:
@@ -700,6 +700,10 @@ def test_relaunch_kill_status_revives_instead_of_kicking(drv):
     assert calls == ["revive", "kick"]
     # a replaced task's end arrives after its successor was stored (unknown task): a full cycle,
     # and a revive so the master offers the stale reservations for release even if we are idle
+    # a FINISH/ONCE task that finished released reservations its pod's next step may reuse
+    calls.clear()
+    fs.status_update(drv, _status("t4", P.TASK_FINISHED))
+    assert calls == ["kick", "revive"]
     calls.clear()
     fs.client = Unknown()
     task_killer.kill_task(P.TaskID(value="t3"), relaunch=True)
