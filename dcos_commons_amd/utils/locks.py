@@ -29,11 +29,11 @@ _held = threading.local()
 
 
 def _held_stack() -> List[int]:
-    st = getattr(_held, "stack", None)
-    if st is None:
-        st = []
-        _held.stack = st
-    return st
+    try:
+        return _held.stack
+    except AttributeError:
+        st = _held.stack = []
+        return st
 
 
 def _reachable(src: int, dst: int) -> Optional[List[int]]:
@@ -72,65 +72,69 @@ def raising_policy(message: str) -> None:
     raise PotentialDeadlockError(message)
 
 
-class _OrderTracker:
-    def __init__(self, name: str, check: bool):
-        self.lock_id = next(_ids)
-        self.check = check
-        _names[self.lock_id] = name
-
-    def before_acquire(self) -> None:
-        if not self.check:
-            return
-        stack = _held_stack()
-        if not stack or self.lock_id in stack:
-            return
-        # Fast path: every held -> this edge is already known (and was cycle-checked when it was
-        # added). Set membership reads are atomic under the GIL, so no graph lock is needed.
-        lid = self.lock_id
-        if all(lid in _edges.get(held, ()) for held in stack):
-            return
-        with _graph_lock:
-            for held in stack:
-                if self.lock_id in _edges.get(held, ()):
-                    continue
-                path = _reachable(self.lock_id, held)
-                if path is not None:
-                    names = " -> ".join(_names[i] for i in path + [self.lock_id])
-                    msg = f"Lock-order cycle detected acquiring {_names[self.lock_id]}: {names}"
-                    break
-                _edges.setdefault(held, set()).add(self.lock_id)
-            else:
-                msg = None
-        if msg:
-            _policy(msg)
-
-    def acquired(self) -> None:
-        _held_stack().append(self.lock_id)
-
-    def released(self) -> None:
-        stack = _held_stack()
-        for i in range(len(stack) - 1, -1, -1):
-            if stack[i] == self.lock_id:
-                del stack[i]
+def _check_order(lock_id: int, stack: List[int]) -> None:
+    """Acquiring ``lock_id`` while holding ``stack`` (non-empty, without ``lock_id``): record the
+    held -> acquired edges, and run the policy if one would close a cycle."""
+    # Fast path: every held -> this edge is already known (and was cycle-checked when it was
+    # added). Set membership reads are atomic under the GIL, so no graph lock is needed.
+    for held in stack:
+        known = _edges.get(held)
+        if known is None or lock_id not in known:
+            break
+    else:
+        return
+    msg = None
+    with _graph_lock:
+        for held in stack:
+            if lock_id in _edges.get(held, ()):
+                continue
+            path = _reachable(lock_id, held)
+            if path is not None:
+                names = " -> ".join(_names[i] for i in path + [lock_id])
+                msg = f"Lock-order cycle detected acquiring {_names[lock_id]}: {names}"
                 break
+            _edges.setdefault(held, set()).add(lock_id)
+    if msg:
+        _policy(msg)
+
+
+def _release_id(stack: List[int], lock_id: int) -> None:
+    if stack and stack[-1] == lock_id:
+        stack.pop()
+        return
+    for i in range(len(stack) - 1, -1, -1):
+        if stack[i] == lock_id:
+            del stack[i]
+            return
+
+
+def _new_id(name: str) -> int:
+    lock_id = next(_ids)
+    _names[lock_id] = name
+    return lock_id
 
 
 class CycleDetectingLock:
     """Re-entrant lock with lock-order cycle detection."""
 
+    __slots__ = ("_lock", "_id", "_check")
+
     def __init__(self, name: str, check: bool = True):
         self._lock = threading.RLock()
-        self._tracker = _OrderTracker(name, check)
+        self._id = _new_id(name)
+        self._check = check
 
     def acquire(self, blocking: bool = True, timeout: float = -1) -> bool:
-        self._tracker.before_acquire()
+        stack = _held_stack()
+        if self._check and stack and self._id not in stack:
+            _check_order(self._id, stack)
         ok = self._lock.acquire(blocking, timeout)
         if ok:
-            self._tracker.acquired()
+            stack.append(self._id)
         return ok
 
     def release(self) -> None:
-        self._tracker.released()
+        _release_id(_held_stack(), self._id)
         self._lock.release()
 
     def __enter__(self):
@@ -142,21 +146,11 @@ class CycleDetectingLock:
 
 
 class _RWView:
+    __slots__ = ("acquire", "release")
+
     def __init__(self, owner: "CycleDetectingRWLock", write: bool):
-        self._owner = owner
-        self._write = write
-
-    def acquire(self) -> None:
-        if self._write:
-            self._owner.acquire_write()
-        else:
-            self._owner.acquire_read()
-
-    def release(self) -> None:
-        if self._write:
-            self._owner.release_write()
-        else:
-            self._owner.release_read()
+        self.acquire = owner.acquire_write if write else owner.acquire_read
+        self.release = owner.release_write if write else owner.release_read
 
     def __enter__(self):
         self.acquire()
@@ -166,52 +160,66 @@ class _RWView:
         self.release()
 
 
+_get_ident = threading.get_ident
+
+
 class CycleDetectingRWLock:
-    """Readers-writer lock (writer re-entrant, writer may take read) with cycle detection."""
+    """Readers-writer lock (writer re-entrant, writer may take read) with cycle detection.
+
+    The uncontended paths (no writer in the way, nobody waiting) take the internal mutex once
+    through its C-level context manager; only a blocked acquire goes through the condition."""
 
     def __init__(self, name: str, check: bool = True):
-        self._cond = threading.Condition(threading.Lock())
+        self._mutex = threading.Lock()
+        self._cond = threading.Condition(self._mutex)
         self._readers: Dict[int, int] = {}
         self._writer: Optional[int] = None
         self._write_depth = 0
-        self._tracker = _OrderTracker(name, check)
+        self._id = _new_id(name)
+        self._check = check
         self._waiting = 0  # threads blocked in _cond.wait(): release only notifies when > 0
         self.read_lock = _RWView(self, False)
         self.write_lock = _RWView(self, True)
 
     def acquire_read(self) -> None:
-        self._tracker.before_acquire()
-        me = threading.get_ident()
-        with self._cond:
+        stack = _held_stack()
+        if self._check and stack and self._id not in stack:
+            _check_order(self._id, stack)
+        me = _get_ident()
+        with self._mutex:
             while self._writer is not None and self._writer != me:
                 self._waiting += 1
                 try:
                     self._cond.wait()
                 finally:
                     self._waiting -= 1
-            self._readers[me] = self._readers.get(me, 0) + 1
-        self._tracker.acquired()
+            readers = self._readers
+            readers[me] = readers.get(me, 0) + 1
+        stack.append(self._id)
 
     def release_read(self) -> None:
-        me = threading.get_ident()
-        self._tracker.released()
-        with self._cond:
-            n = self._readers.get(me, 0) - 1
+        me = _get_ident()
+        _release_id(_held_stack(), self._id)
+        with self._mutex:
+            readers = self._readers
+            n = readers.get(me, 0) - 1
             if n <= 0:
-                self._readers.pop(me, None)
+                readers.pop(me, None)
             else:
-                self._readers[me] = n
+                readers[me] = n
             if self._waiting:
                 self._cond.notify_all()
 
     def acquire_write(self) -> None:
-        self._tracker.before_acquire()
-        me = threading.get_ident()
-        with self._cond:
+        stack = _held_stack()
+        if self._check and stack and self._id not in stack:
+            _check_order(self._id, stack)
+        me = _get_ident()
+        with self._mutex:
             if self._writer == me:
                 self._write_depth += 1
             else:
-                while self._writer is not None or any(t != me for t in self._readers):
+                while self._writer is not None or (self._readers and any(t != me for t in self._readers)):
                     self._waiting += 1
                     try:
                         self._cond.wait()
@@ -219,11 +227,11 @@ class CycleDetectingRWLock:
                         self._waiting -= 1
                 self._writer = me
                 self._write_depth = 1
-        self._tracker.acquired()
+        stack.append(self._id)
 
     def release_write(self) -> None:
-        self._tracker.released()
-        with self._cond:
+        _release_id(_held_stack(), self._id)
+        with self._mutex:
             self._write_depth -= 1
             if self._write_depth == 0:
                 self._writer = None
