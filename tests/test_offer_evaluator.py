@@ -557,3 +557,22 @@ def test_same_cycle_placement_sees_pods_matched_earlier_in_the_cycle():
     assert len(launches) == 2
     assert sorted(TaskLabelReader(l.task_info).get_offer_attribute_strings()[0] for l in launches) == \
         ["rack:r1", "rack:r2"]
+
+
+def test_in_place_relaunch_skips_offers_without_its_reservations():
+    """An offer lacking a reservation the existing pipeline consumes by ID fails without running
+    the stages (one ``ReservationPrecheck`` outcome is tracked); the offer that carries them is
+    evaluated as usual, whatever its position."""
+    from dcos_commons_amd.offer.history import OfferOutcomeTracker
+
+    f = Fixture(server(1.0, 32))
+    first = f.launch([complete_offer(scalar("cpus", 2.0), scalar("mem", 64))])
+    f.evaluator.offer_outcome_tracker = OfferOutcomeTracker()
+    other_agent = complete_offer(scalar("cpus", 8.0), scalar("mem", 640), oid="other", agent="a-other")
+    partial = offer(*(_executor_reserved(first) + [_reserved(first, "cpus")]), oid="partial")
+    assert f.evaluate([other_agent, partial]) == []
+    text = str(f.evaluator.offer_outcome_tracker.to_json())
+    assert text.count("ReservationPrecheck") == 2 and "lacks 2 of the 2" in text and "lacks 1 of the 2" in text
+    full = offer(*(_executor_reserved(first) + [_reserved(first, "cpus"), _reserved(first, "mem")]), oid="full")
+    again = f.evaluate([other_agent, full])
+    assert ops(again) == [L, None] and again[0].offer.id.value == "full"
