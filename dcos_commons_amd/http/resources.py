@@ -413,7 +413,8 @@ class PodResource:
     @staticmethod
     def _kill(name: str, tasks) -> Response:
         for info, _ in tasks:
-            task_killer.kill_task(info.task_id)
+            if info.task_id.value:  # a footprint placeholder was never launched: nothing to kill
+                task_killer.kill_task(info.task_id)
         return json_ok({"pod": name, "tasks": [info.name for info, _ in tasks]})
 
 

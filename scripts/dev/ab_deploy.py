@@ -1,6 +1,6 @@
 """python scripts/dev/ab_deploy.py <repo> <n> <cycles>: helloworld DeployBench of the tree at <repo>, synthetic readiness (0.2 ms GIL-free sleep), pinned to CPUs 4-7; prints mean/median deploy, MTTRs and process CPU per cycle."""
 import sys, os, time, json, logging
-repo=sys.argv[1]; sys.path.insert(0, repo); os.chdir(repo)
+repo=os.path.abspath(sys.argv[1]); sys.path.insert(0, repo); os.chdir(repo)
 logging.disable(logging.WARNING)
 os.sched_setaffinity(0,[4,5,6,7])
 from dcos_commons_amd.benchmarks.deploy_bench import DeployBench
