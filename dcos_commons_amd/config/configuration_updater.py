@@ -14,12 +14,7 @@ from typing import List, Optional
 
 from dcos_commons_amd.mesos import protos as P
 from dcos_commons_amd.offer.taskdata.labels import TaskException, TaskLabelReader, TaskLabelWriter
-from dcos_commons_amd.specification.specs import (
-    DEFAULT_SERVICE_USER,
-    ResourceSet,
-    ResourceSpec,
-    VolumeSpec,
-)
+from dcos_commons_amd.specification.specs import DEFAULT_SERVICE_USER, ResourceSet, ResourceSpec
 from dcos_commons_amd.state.config_store import ConfigStoreException
 from dcos_commons_amd.storage.persister import Reason
 

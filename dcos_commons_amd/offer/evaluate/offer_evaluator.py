@@ -12,7 +12,6 @@ pass a pre-fetched task map (``all_tasks``) so a whole offer cycle touches stora
 """
 from __future__ import annotations
 
-import logging
 from typing import Dict, List, Optional, Sequence
 
 from dcos_commons_amd import trace

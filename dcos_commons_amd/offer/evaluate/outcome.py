@@ -4,7 +4,7 @@ Reference: sdk/.../offer/evaluate/EvaluationOutcome.java:17-216.
 """
 from __future__ import annotations
 
-from typing import Any, List, Optional
+from typing import Any, List
 
 
 class EvaluationOutcome:

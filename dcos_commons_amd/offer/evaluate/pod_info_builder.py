@@ -5,10 +5,8 @@ here; ``LaunchEvaluationStage`` snapshots them into launch / store recommendatio
 """
 from __future__ import annotations
 
-import uuid
 from typing import Dict, List, Optional, Set
 
-from dcos_commons_amd.dcos import constants as dcos
 from dcos_commons_amd.http import endpoint_utils as eu
 from dcos_commons_amd.mesos import protos as P
 from dcos_commons_amd.offer import common_id_utils

@@ -10,8 +10,7 @@ recommendations.
 from __future__ import annotations
 
 import logging
-from dataclasses import replace
-from typing import Collection, List, Optional
+from typing import Collection, Optional
 
 from dcos_commons_amd.dcos import constants as dcos
 from dcos_commons_amd.mesos import protos as P

@@ -9,7 +9,7 @@ import collections
 import html
 import threading
 import time
-from typing import Dict, List
+from typing import Dict
 
 from dcos_commons_amd.mesos import protos as P
 

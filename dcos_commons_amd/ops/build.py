@@ -13,7 +13,7 @@ import os
 import shutil
 import subprocess
 import sys
-from typing import List, Optional
+from typing import List
 
 ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 OPS = os.path.join(ROOT, "dcos_commons_amd", "ops")

@@ -7,8 +7,7 @@ unexpected-reservation garbage collector and status-update processing.
 """
 from __future__ import annotations
 
-import logging
-from typing import Dict, List, Optional
+from typing import Dict, Optional
 
 from dcos_commons_amd.framework import task_killer
 from dcos_commons_amd.http import endpoint_utils

@@ -6,7 +6,7 @@ sdk/.../scheduler/OfferResources.java.
 from __future__ import annotations
 
 import enum
-from typing import Collection, List, Optional
+from typing import List
 
 from dcos_commons_amd.mesos import protos as P
 

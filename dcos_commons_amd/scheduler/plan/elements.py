@@ -9,7 +9,7 @@ from __future__ import annotations
 import logging
 import threading
 import uuid
-from typing import Collection, Dict, Iterable, List, Optional, Set
+from typing import Dict, Iterable, List, Optional, Set
 
 from dcos_commons_amd.offer import constants
 from dcos_commons_amd.scheduler.plan import backoff as backoff_mod

@@ -14,7 +14,7 @@ step is evaluated (with or without launch streaming).
 from __future__ import annotations
 
 import logging
-from typing import List, Optional
+from typing import Optional
 
 from dcos_commons_amd.framework import task_killer
 from dcos_commons_amd.offer.recommendations import StoreTaskInfoRecommendation

@@ -40,7 +40,7 @@ from dcos_commons_amd.scheduler.recovery import (
 )
 from dcos_commons_amd.offer.task_utils import has_tasks_with_tls
 from dcos_commons_amd.scheduler.uninstall import UninstallScheduler
-from dcos_commons_amd.specification.specs import ServiceSpec, ServiceSpecFactory, loopback_check
+from dcos_commons_amd.specification.specs import ServiceSpec, loopback_check
 from dcos_commons_amd.state import state_store_utils
 from dcos_commons_amd.state.config_store import ConfigStore, ConfigStoreException
 from dcos_commons_amd.state.framework_store import FrameworkStore

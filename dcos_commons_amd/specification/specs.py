@@ -18,7 +18,7 @@ import enum
 import functools
 import json
 import re
-from dataclasses import dataclass, field, replace
+from dataclasses import dataclass, replace
 from typing import Any, Dict, List, Optional, Tuple
 
 from dcos_commons_amd.mesos import protos as P

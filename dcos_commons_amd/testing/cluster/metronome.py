@@ -14,7 +14,7 @@ import tempfile
 import threading
 import time
 import uuid
-from typing import Dict, List, Optional
+from typing import Dict, List
 
 
 class LocalMetronome:

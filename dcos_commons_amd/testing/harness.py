@@ -15,7 +15,7 @@ from dcos_commons_amd.framework.process_exit import ProcessExit
 from dcos_commons_amd.http.api import Router
 from dcos_commons_amd.mesos import protos as P
 from dcos_commons_amd.offer.resources import get_resource_id
-from dcos_commons_amd.offer.taskdata.labels import TaskLabelReader, env_to_map
+from dcos_commons_amd.offer.taskdata.labels import env_to_map
 from dcos_commons_amd.scheduler.plan.status import Status
 from dcos_commons_amd.scheduler.scheduler_builder import SchedulerBuilder
 from dcos_commons_amd.scheduler.scheduler_config import SchedulerConfig

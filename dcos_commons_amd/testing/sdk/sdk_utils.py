@@ -12,7 +12,7 @@ import logging
 import os
 import random
 import string
-from typing import Any, Dict, List
+from typing import Any, Dict
 
 LOG = logging.getLogger(__name__)
 
