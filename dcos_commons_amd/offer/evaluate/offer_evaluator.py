@@ -141,6 +141,8 @@ class OfferEvaluator:
         fid_proto = self._fid()
         if self._framework_id is None:
             self._framework_id = fid_proto.value
+        if not offers:
+            return []  # nothing to match: the pipeline would be built for no offer
         if all_tasks is None:
             all_tasks = {t.name: t for t in self.state_store.fetch_tasks()}
         pi = requirement.pod_instance
