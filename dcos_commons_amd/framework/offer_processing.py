@@ -466,10 +466,13 @@ class OfferProcessor:
         self._in_progress = set()
         self._in_progress_lock = threading.Lock()
         self._wake = threading.Event()
-        # why the loop was woken: ``kick`` asks for a full cycle; ``reoffer_released`` for a revive
-        # (both are read and reset by the offer thread at the start of a cycle)
-        self._eval_wake = False
-        self._reoffer = False
+        # why the loop was woken: ``kick`` asks for a full cycle, ``reoffer_released`` for a revive.
+        # Requests bump a counter; the offer thread compares it with the value it last acted on,
+        # so a request made while it reads is seen on the next cycle instead of being reset away.
+        self._eval_requests = 0
+        self._reoffer_requests = 0
+        self._eval_seen = 0
+        self._reoffer_seen = 0
         # after a revive-only wake-up, a full cycle runs at this time unless an offer or a kick
         # brings one sooner (a kill of a task the master did not know frees nothing to re-offer)
         self._fallback_cycle_at: Optional[float] = None
@@ -518,7 +521,7 @@ class OfferProcessor:
     def kick(self) -> None:
         """Wake the loop now (status update / plan change) instead of at the next offer poll."""
         if self.event_driven:
-            self._eval_wake = True
+            self._eval_requests += 1
             self._wake.set()
             self.queue.notify()
 
@@ -530,7 +533,7 @@ class OfferProcessor:
         floor. The offer that carries them wakes the loop for the relaunch. The revive is taken on
         the offer thread, like every revive (OfferProcessor.java:300-309)."""
         if self.event_driven:
-            self._reoffer = True
+            self._reoffer_requests += 1
             self._wake.set()
             self.queue.notify()
 
@@ -574,8 +577,10 @@ class OfferProcessor:
         new_offers = self.queue.take_all(wait_s, self._wake if self.event_driven else None)
         if self._stop.is_set():
             return
-        reoffer, self._reoffer = self._reoffer, False
-        eval_wake, self._eval_wake = self._eval_wake, False
+        seen, self._reoffer_seen = self._reoffer_seen, self._reoffer_requests
+        reoffer = seen != self._reoffer_seen
+        seen, self._eval_seen = self._eval_seen, self._eval_requests
+        eval_wake = seen != self._eval_seen
         if reoffer and not new_offers and not eval_wake:
             self.revive_manager.request_revive(bypass_spacing=True)
             self.revive_manager.revive_if_requested()
@@ -608,7 +613,7 @@ class OfferProcessor:
                             self.client.consume_recheck_request():
                         # the client started work that changes its status (e.g. uninstall's
                         # deregister step): re-check now rather than at the next offer poll
-                        self._eval_wake = True
+                        self._eval_requests += 1
                         self._wake.set()
                 elif self._deregistered:
                     # the framework was just torn down: its offers went with it

@@ -667,7 +667,7 @@ def test_reoffer_wakes_for_a_revive_only(drv):
     # without event-driven wake-ups (the reference cadence) nothing is requested
     q = processor(CountingClient())
     q.reoffer_released()
-    assert not q._reoffer
+    assert q._reoffer_requests == 0
 
 
 def test_relaunch_kill_status_revives_instead_of_kicking(drv):
