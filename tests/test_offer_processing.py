@@ -157,3 +157,15 @@ def test_accepter_names_every_member_offer():
         driver.set_driver(None)
     assert calls == [["o1", "o2"]]
 
+
+
+def test_cluster_bench_cycle():
+    """The cluster-mode bench: scheduler process + v1 HTTP API + ZooKeeper, real task processes."""
+    from dcos_commons_amd.benchmarks.cluster_bench import ClusterBench
+
+    b = ClusterBench(agents=2, timeout_s=60.0)
+    try:
+        r = b.run_cycle()
+    finally:
+        b.close()
+    assert 0 < r["deploy_s"] < 30 and 0 < r["mttr_restart_s"] < 30 and 0 < r["mttr_replace_s"] < 30
