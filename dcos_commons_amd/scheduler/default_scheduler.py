@@ -285,15 +285,15 @@ class DefaultScheduler(AbstractScheduler):
             self.logger.warning("Launch of %s never reached the master (%s, %s): relaunching with new reservations",
                                 name, P.TaskState.Name(status.state), P.TaskStatus.Reason.Name(status.reason))
             set_permanently_failed(self.state_store, [info])
-        self.state_store.store_status(name, status)
-        for pm in self.plan_coordinator.get_plan_managers():
-            pm.update(status)
+        # a status carrying IP addresses is also kept as the `<task>:task-status` property
+        # (StateStoreUtils.storeTaskStatusAsProperty), written in the same transaction
+        props = None
         if status.HasField("container_status") and any(
                 len(ni.ip_addresses) > 0 for ni in status.container_status.network_infos):
-            try:
-                state_store_utils.store_task_status_as_property(self.state_store, name, status)
-            except Exception as e:  # noqa: BLE001
-                self.logger.warning("Unable to store network info for status update: %s", e)
+            props = {name + state_store_utils.PROPERTY_TASK_INFO_SUFFIX: status.SerializeToString()}
+        self.state_store.store_status(name, status, props)
+        for pm in self.plan_coordinator.get_plan_managers():
+            pm.update(status)
 
     def to_uninstall_scheduler(self):
         from dcos_commons_amd.scheduler.uninstall import UninstallScheduler

@@ -126,7 +126,10 @@ class StateStore:
             except PersisterException as e:
                 raise StateStoreException(e.reason, f"Failed to store {len(b)} TaskInfos") from e
 
-    def store_status(self, task_name: str, status: P.TaskStatus) -> None:
+    def store_status(self, task_name: str, status: P.TaskStatus,
+                     properties: Optional[Dict[str, bytes]] = None) -> None:
+        """Stores ``status`` (StateStore.storeStatus). ``properties`` are written in the same
+        persister transaction (one ZooKeeper multi instead of a round trip each)."""
         current = self.fetch_status(task_name)
         from dcos_commons_amd.offer.task_utils import is_terminal
 
@@ -140,7 +143,15 @@ class StateStore:
             raise StateStoreException(Reason.NOT_FOUND,
                                       f"Dropping TaskStatus with unknown TaskID: {status.task_id.value}")
         try:
-            self.persister.set(self._task_status_path(task_name), status.SerializeToString())
+            if properties:
+                m = {self._task_status_path(task_name): status.SerializeToString()}
+                for k, v in properties.items():
+                    self._validate_key(k)
+                    self._validate_value(v)
+                    m[self._property_path(k)] = v
+                self.persister.set_many(m)
+            else:
+                self.persister.set(self._task_status_path(task_name), status.SerializeToString())
         except PersisterException as e:
             raise StateStoreException(e.reason, str(e)) from e
 
