@@ -107,19 +107,26 @@ class ZooKeeperPersister(Persister):
 
     # -- writes -------------------------------------------------------------------------
     def set(self, path: str, data: Optional[bytes]) -> None:
+        """setData on the node, creating it (and its parents) when it does not exist yet
+        (CuratorPersister.set). The common case, an existing node, is one round trip: the write
+        is tried first and the creation path only runs on NoNode."""
         p = self._p(path)
         try:
-            if self.client.exists(p) is not None:
-                if self.client.get(p)[0] != data:
-                    self.client.set(p, data)
-            else:
-                for parent in get_parent_paths(p):
-                    if self.client.exists(parent) is None:
-                        try:
-                            self.client.create(parent)
-                        except Z.NodeExistsError:
-                            pass
+            try:
+                self.client.set(p, data)
+                return
+            except Z.NoNodeError:
+                pass
+            for parent in get_parent_paths(p):
+                if self.client.exists(parent) is None:
+                    try:
+                        self.client.create(parent)
+                    except Z.NodeExistsError:
+                        pass
+            try:
                 self.client.create(p, data)
+            except Z.NodeExistsError:
+                self.client.set(p, data)  # created concurrently since the failed setData
         except Z.ZkError as e:
             raise self._storage_error(f"Unable to set {len(data or b'')} bytes in {p}", e)
 
@@ -139,9 +146,21 @@ class ZooKeeperPersister(Persister):
             self.client.ensure_path(self.root)
 
     def set_many(self, path_bytes: Mapping[str, Optional[bytes]]) -> None:
+        """One transaction (CuratorPersister.setMany): setData on existing nodes, creates for
+        missing ones and their parents. It is first tried as setData only, which is one round
+        trip when every node exists (status updates, relaunches); a transaction that fails on a
+        missing node is rebuilt with existence checks, as the reference always does."""
         if not path_bytes:
             return
         prefixed = {self._p(k): v for k, v in sorted(path_bytes.items())}
+        try:
+            self.client.multi([Z.Check(self.root)] + [Z.SetData(p, d) for p, d in prefixed.items()])
+            return
+        except Z.TransactionError as e:
+            if not isinstance(e.failed, Z.NoNodeError):
+                LOGGER.info("Optimistic setData transaction failed (%s): rebuilding it", e)
+        except Z.ZkError as e:
+            LOGGER.info("Optimistic setData transaction failed (%s): rebuilding it", e)
         try:
             self._ensure_root()
         except Z.ZkError as e:
