@@ -24,6 +24,7 @@ Wire formats: ``application/x-protobuf`` (default; binary-compatible with the Me
 from __future__ import annotations
 
 import base64
+import collections
 import http.client
 import json
 import logging
@@ -71,7 +72,8 @@ class V1HttpSchedulerDriver(SchedulerDriver):
                  credential: Optional[P.Credential] = None, content_type: str = PROTOBUF,
                  implicit_acknowledgements: bool = True, reconnect: bool = False,
                  heartbeat_misses: int = 5, connect_timeout_s: float = 10.0,
-                 backoff_s: float = 0.5, max_backoff_s: float = 10.0, token_provider=None):
+                 backoff_s: float = 0.5, max_backoff_s: float = 10.0, token_provider=None,
+                 async_calls: bool = False):
         if content_type not in (PROTOBUF, JSON):
             raise ValueError(f"unsupported content type {content_type}")
         self.master_url = master_url.rstrip("/")
@@ -101,6 +103,15 @@ class V1HttpSchedulerDriver(SchedulerDriver):
         self._conns_lock = threading.Lock()
         self.exit_status = 0
         self._tearing_down = False
+        # async_calls: calls are POSTed in submission order by one sender thread and the caller
+        # returns at once, like the reference's libprocess-backed driver (a call's outcome is
+        # logged, not raised). The offer thread then does not wait for an ACCEPT's HTTP round trip,
+        # nor the event stream for an ACKNOWLEDGE's before it reads the next event.
+        self.async_calls = async_calls
+        self._outbox: "collections.deque[P.Call]" = collections.deque()
+        self._outbox_cond = threading.Condition()
+        self._in_flight = 0
+        self._sender: Optional[threading.Thread] = None
 
     # -- lifecycle ---------------------------------------------------------------------
     @property
@@ -127,9 +138,10 @@ class V1HttpSchedulerDriver(SchedulerDriver):
     def stop(self, failover: bool = True) -> None:
         if self._stopped.is_set():
             return
+        self.flush()
         if not failover and self._framework_id and self.stream_id and not self._tearing_down:
             try:
-                self._send(P.Call(type=P.Call.TEARDOWN))
+                self._send_now(P.Call(type=P.Call.TEARDOWN))
             except Exception as e:  # noqa: BLE001
                 LOGGER.warning("TEARDOWN on stop failed: %s", e)
         self._stopped.set()
@@ -200,7 +212,8 @@ class V1HttpSchedulerDriver(SchedulerDriver):
     def teardown(self) -> None:
         # the master ends the event stream in answer: that is not a disconnection
         self._tearing_down = True
-        self._send(P.Call(type=P.Call.TEARDOWN))
+        self.flush()
+        self._send_now(P.Call(type=P.Call.TEARDOWN))
 
     # -- transport ---------------------------------------------------------------------
     def _headers(self, accept: str) -> dict:
@@ -232,6 +245,48 @@ class V1HttpSchedulerDriver(SchedulerDriver):
         return conn
 
     def _send(self, call: P.Call) -> None:
+        if not self.async_calls:
+            self._send_now(call)
+            return
+        with self._outbox_cond:
+            self._outbox.append(call)
+            if self._sender is None:
+                self._sender = threading.Thread(target=self._send_loop, name="mesos-v1-calls", daemon=True)
+                self._sender.start()
+            self._outbox_cond.notify()
+
+    def _send_loop(self) -> None:
+        while True:
+            with self._outbox_cond:
+                while not self._outbox:
+                    if self._stopped.is_set():
+                        return
+                    self._outbox_cond.wait(0.5)
+                call = self._outbox.popleft()
+                self._in_flight += 1
+            try:
+                self._send_now(call)
+            except Exception as e:  # noqa: BLE001 -- the caller has moved on: report, keep sending
+                LOGGER.error("Mesos %s call failed: %s", P.Call.Type.Name(call.type), e)
+            finally:
+                with self._outbox_cond:
+                    self._in_flight -= 1
+                    self._outbox_cond.notify_all()
+
+    def flush(self, timeout_s: float = 10.0) -> bool:
+        """Waits until every call submitted so far has been sent (async mode); True if it was."""
+        if not self.async_calls:
+            return True
+        deadline = time.monotonic() + timeout_s
+        with self._outbox_cond:
+            while self._outbox or self._in_flight:
+                left = deadline - time.monotonic()
+                if left <= 0 or self._sender is None or not self._sender.is_alive():
+                    return False
+                self._outbox_cond.wait(min(left, 0.05))
+        return True
+
+    def _send_now(self, call: P.Call) -> None:
         if self._framework_id:
             call.framework_id.value = self._framework_id
         if self.stream_id is None:

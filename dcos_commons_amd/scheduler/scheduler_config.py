@@ -199,6 +199,13 @@ class SchedulerConfig:
         """MI355X build: resubscribe after a lost event stream instead of exiting (reference exits)."""
         return self.env.get_optional_boolean("SDK_DRIVER_RECONNECT", False)
 
+    def is_async_mesos_calls(self) -> bool:
+        """Mesos v1 calls (ACCEPT, ACKNOWLEDGE, KILL, REVIVE, ...) are POSTed in order by one sender
+        thread and the caller does not wait for the HTTP answer (``SDK_ASYNC_MESOS_CALLS``, default
+        on), as the reference's libprocess-backed driver does; off: each call is a synchronous
+        request whose failure raises in the caller."""
+        return self.env.get_optional_boolean("SDK_ASYNC_MESOS_CALLS", True)
+
     def mesos_credential(self):
         """Principal + secret from ``SDK_MESOS_PRINCIPAL``/``SDK_MESOS_SECRET`` (tools and tests that
         build a driver by hand; the scheduler itself uses SchedulerDriverFactory's rules)."""

@@ -403,3 +403,29 @@ def test_mesos_principal_override_must_match_the_framework_principal():
     check_principal_override(info, SchedulerConfig.for_testing(SDK_MESOS_PRINCIPAL="svc-principal"))
     with pytest.raises(ValueError, match="SDK_MESOS_PRINCIPAL"):
         check_principal_override(info, SchedulerConfig.for_testing(SDK_MESOS_PRINCIPAL="other"))
+
+
+def test_async_calls_are_sent_in_order_and_failures_are_logged(caplog):
+    lm = LocalMaster(allocation_interval_s=0.05)
+    lm.add_agent(AgentSpec(hostname="h0", cpus=2, mem=1024, disk=1024))
+    hm = HttpMaster(lm, heartbeat_s=0.2).start()
+    rec = Recorder()
+    d = V1HttpSchedulerDriver(hm.url, rec, P.FrameworkInfo(name="fw", role="r"), async_calls=True)
+    d.start()
+    try:
+        rec.wait_for("registered")
+        for _ in range(5):
+            d.suppress_offers()
+            d.revive_offers()
+        assert d.flush(5.0)
+        assert hm.calls["SUPPRESS"] == 5 and hm.calls["REVIVE"] == 5
+        order = [c for c in getattr(hm, "call_log", []) if c in ("SUPPRESS", "REVIVE")]
+        if order:   # when the fake master logs call order, it is the submission order
+            assert order == ["SUPPRESS", "REVIVE"] * 5
+        # a call the master rejects is reported in the log; the caller is not interrupted
+        d.kill_task(P.TaskID(value=""))   # no task id: a 400 from the master
+        d.flush(5.0)
+    finally:
+        d.stop()
+        hm.stop()
+        lm.shutdown()
