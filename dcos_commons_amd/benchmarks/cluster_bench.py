@@ -114,7 +114,8 @@ class ClusterBench:
         self.timeout_s = timeout_s
         env = {"SDK_LOCK_WAIT_S": "1"}
         env.update(profile_env or {})
-        self.cluster = LocalCluster(agents=agents, gpus_per_agent=1, executor=executor,
+        # ZooKeeper in its own process, as on a cluster (the master and agents stay in this one)
+        self.cluster = LocalCluster(agents=agents, gpus_per_agent=1, executor=executor, zk_process=True,
                                     allocation_interval_s=allocation_interval_s, scheduler_env=env).start()
         use(self.cluster)
         self.watch = _Watch(self.cluster)

@@ -44,6 +44,54 @@ DEFAULT_ZONES = ("us-west-2a", "us-west-2b", "us-west-2c")
 # services (ZooKeeper 2181/3888, Mesos agent 5051, adminrouter 8080-8081, ...)
 DCOS_AGENT_PORTS = ((1025, 2180), (2182, 3887), (3889, 5049), (5052, 8079), (8082, 8180), (8182, 32000))
 
+class _ZkProcess:
+    """The ZooKeeper stand-in in its own interpreter (``python -m dcos_commons_amd.testing.zk_server``),
+    as ZooKeeper is its own JVM on a cluster: its request handling then does not share the GIL
+    with the master, the agents and the bench driving them. Connection drops are not supported."""
+
+    def __init__(self):
+        self.proc = None
+        self.port = 0
+
+    @property
+    def connect_string(self) -> str:
+        return f"127.0.0.1:{self.port}"
+
+    def start(self) -> "_ZkProcess":
+        import socket
+        import subprocess
+        import sys
+
+        from dcos_commons_amd.testing.cluster.marathon import REPO_ROOT, free_port
+
+        self.port = free_port()
+        env = dict(os.environ, PYTHONPATH=REPO_ROOT)
+        self.proc = subprocess.Popen([sys.executable, "-m", "dcos_commons_amd.testing.zk_server", "--port",
+                                      str(self.port)], env=env, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+        deadline = time.monotonic() + 30
+        while True:
+            try:
+                socket.create_connection(("127.0.0.1", self.port), timeout=1).close()
+                return self
+            except OSError:
+                if self.proc.poll() is not None or time.monotonic() > deadline:
+                    self.stop()
+                    raise RuntimeError("the ZooKeeper stand-in process did not start")
+                time.sleep(0.05)
+
+    def drop_connections(self) -> None:
+        raise NotImplementedError("connection drops need the in-process ZooKeeper stand-in")
+
+    def stop(self) -> None:
+        if self.proc is not None and self.proc.poll() is None:
+            self.proc.terminate()
+            try:
+                self.proc.wait(5)
+            except Exception:  # noqa: BLE001
+                self.proc.kill()
+                self.proc.wait(5)
+
+
 _current: Optional["LocalCluster"] = None
 _current_lock = threading.Lock()
 
@@ -100,7 +148,7 @@ class LocalCluster:
                  agent_cpus: float = 8.0, agent_mem: float = 32768.0, agent_disk: float = 65536.0,
                  packages: Optional[Dict[str, str]] = None, scheduler_env: Optional[Dict[str, str]] = None,
                  finish_tasks: Sequence[str] = (), dcos_version: str = "1.13.0", keep_work_dir: bool = False,
-                 mount_disks: Sequence[tuple] = (), dcos_security: bool = False):
+                 mount_disks: Sequence[tuple] = (), dcos_security: bool = False, zk_process: bool = False):
         self.work_dir = os.path.abspath(work_dir or tempfile.mkdtemp(prefix="sdk-cluster-"))
         self._own_work_dir = work_dir is None and not keep_work_dir
         self.region = region
@@ -152,7 +200,8 @@ class LocalCluster:
         self._tasks: Dict[str, TaskView] = {}
         self._tasks_lock = threading.Lock()
         self.agent_ids: Dict[str, str] = {}  # hostname -> agent id
-        self.zk: Optional[ZkServer] = None
+        self.zk = None  # ZkServer, or a _ZkProcess with zk_process=True
+        self.zk_process = zk_process
         self.http_master: Optional[HttpMaster] = None
         self.marathon = LocalMarathon(self)
         from dcos_commons_amd.testing.cluster.metronome import LocalMetronome
@@ -165,7 +214,7 @@ class LocalCluster:
     def start(self) -> "LocalCluster":
         if self.dcos is not None:
             self.dcos.start()
-        self.zk = ZkServer().start()
+        self.zk = _ZkProcess().start() if self.zk_process else ZkServer().start()
         self.http_master = HttpMaster(self.master).start()
         for spec in self._agent_specs:
             self.agent_ids[spec.hostname] = self.master.add_agent(spec)
