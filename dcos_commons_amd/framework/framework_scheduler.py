@@ -26,6 +26,9 @@ from .process_exit import ProcessExit
 LOGGER = logging.getLogger(__name__)
 
 _NO_NEW_WORK_STATES = (P.TASK_STAGING, P.TASK_STARTING)
+# terminal states whose agent has released the task's resources (an unreachable or lost agent
+# releases nothing the master could offer again)
+_RELEASING_STATES = frozenset([P.TASK_FINISHED, P.TASK_FAILED, P.TASK_KILLED, P.TASK_ERROR])
 
 
 def can_create_work(status: P.TaskStatus) -> bool:
@@ -169,18 +172,18 @@ class FrameworkScheduler:
                 else:
                     LOGGER.warning("Received status update for unknown task, but task should not be killed "
                                    "again: %s", status.task_id.value)
-            # A task that ended after a kill issued for a relaunch, or a FINISH/ONCE task that
-            # finished, released reservations the plans reuse. A revive has the master offer them
-            # now: for an in-place relaunch (or the pod's next step) that offer carries what it
-            # needs, and wakes the loop for it (a cycle now would re-evaluate against the offers
-            # in hand, which cannot hold them); for a replacement placed elsewhere it carries the
-            # stale reservations to release, which a scheduler that has gone idle (suppressed)
-            # would otherwise never be offered.
-            finished = status.state == P.TASK_FINISHED and resp.result != TaskStatusResult.UNKNOWN_TASK
+            # A task that ended (finished, failed, killed: after a kill issued for a relaunch
+            # too) released reservations the plans reuse: an in-place relaunch or recovery, or
+            # the pod's next step. A revive has the master offer them now, and that offer wakes
+            # the loop for the relaunch (after a relaunch kill no full cycle runs first: the
+            # offers in hand cannot hold them). For a replacement placed elsewhere the offer
+            # carries the stale reservations to release, which a scheduler that has gone idle
+            # (suppressed) would otherwise never be offered.
+            released = status.state in _RELEASING_STATES and resp.result != TaskStatusResult.UNKNOWN_TASK
             if resp.result == TaskStatusResult.UNKNOWN_TASK or reconciling or \
                     (can_create_work(status) and not relaunch_kill):
                 self.offer_processor.kick()
-            if relaunch_kill or finished:
+            if relaunch_kill or released:
                 self.offer_processor.reoffer_released()
         except Exception as e:  # noqa: BLE001
             self._exit(e)

@@ -230,12 +230,13 @@ class ReviveManager:
         self.revive_requested = False
         self._revive_bypass = False
 
-    def revive_if_requested(self) -> None:
+    def revive_if_requested(self) -> bool:
+        """Revives if a revive is requested and the bucket allows it; True if it did."""
         if not self.revive_requested:
-            return
+            return False
         if not self.bucket.try_acquire(ignore_spacing=self._revive_bypass):
             metrics.increment_revive_throttles()
-            return
+            return False
         d = driver.get_instance()
         if d is not None:
             d.revive_offers()
@@ -243,6 +244,7 @@ class ReviveManager:
         self._revive_bypass = False
         self.is_suppressed = False
         metrics.increment_revives()
+        return True
 
 
 class OfferAccepter:
@@ -582,11 +584,13 @@ class OfferProcessor:
         seen, self._eval_seen = self._eval_seen, self._eval_requests
         eval_wake = seen != self._eval_seen
         if reoffer and not new_offers and not eval_wake:
-            self.revive_manager.request_revive(bypass_spacing=True)
-            self.revive_manager.revive_if_requested()
+            self._reoffer_revive()
             self._fallback_cycle_at = time.monotonic() + REOFFER_FALLBACK_CYCLE_S
             return
         self._fallback_cycle_at = None
+        # released reservations: the REVIVE goes out before the cycle, so the master allocates them
+        # while the cycle runs instead of after it
+        revived_early = reoffer and self._reoffer_revive()
         now = time.monotonic()
         with self._held_lock:
             held = [o for o, _ in self._held.values()]
@@ -626,9 +630,13 @@ class OfferProcessor:
                     if self.gc_all_offers:
                         offers = self._collect_garbage(offers)
                     decline_long(offers)
-            if reoffer:
-                # requested after the cycle's own revive bookkeeping, so neither a suppress nor
-                # a cancelled work-set revive drops it
+            if revived_early:
+                # the master has allocated everything available since that REVIVE: a revive this
+                # cycle asked for (new work) would only repeat it
+                self.revive_manager.cancel_request()
+            elif reoffer:
+                # throttled before the cycle: requested again after the cycle's own revive
+                # bookkeeping, so neither a suppress nor a cancelled work-set revive drops it
                 self.revive_manager.request_revive(bypass_spacing=True)
             self.revive_manager.revive_if_requested()
         finally:
@@ -636,6 +644,10 @@ class OfferProcessor:
             with self._in_progress_lock:
                 for o in new_offers:
                     self._in_progress.discard(o.id.value)
+
+    def _reoffer_revive(self) -> bool:
+        self.revive_manager.request_revive(bypass_spacing=True)
+        return self.revive_manager.revive_if_requested()
 
     def _candidates_all_launched(self) -> bool:
         steps = getattr(self.client, "candidate_steps", None)

@@ -697,7 +697,11 @@ def test_relaunch_kill_status_revives_instead_of_kicking(drv):
     fs.status_update(drv, _status("t1", P.TASK_KILLED))
     task_killer.kill_task(P.TaskID(value="t2"))
     fs.status_update(drv, _status("t2", P.TASK_KILLED))
-    assert calls == ["revive", "kick"]
+    # any other end that releases resources: a cycle for the work it creates, and a re-offer
+    assert calls == ["revive", "kick", "revive"]
+    calls.clear()
+    fs.status_update(drv, _status("t5", P.TASK_LOST))   # an unreachable agent releases nothing
+    assert calls == ["kick"]
     # a replaced task's end arrives after its successor was stored (unknown task): a full cycle,
     # and a revive so the master offers the stale reservations for release even if we are idle
     # a FINISH/ONCE task that finished released reservations its pod's next step may reuse
