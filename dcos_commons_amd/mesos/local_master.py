@@ -319,18 +319,6 @@ class LocalMaster:
             heapq.heappush(self._heap, (self.clock() + max(0.0, delay), next(self._seq), fn, args))
             self._cond.notify()
 
-    def _next(self, delay: float, fn, *args) -> None:
-        """A launched task's first lifecycle step: due now, it runs right after the current action,
-        ahead of actions already queued (the next ACCEPTs of a cycle that streamed its launches):
-        agents start their tasks while the master works through later calls, rather than after
-        every queued ACCEPT has been applied."""
-        if delay <= 0:
-            with self._cond:
-                heapq.heappush(self._heap, (0.0, next(self._seq), fn, args))
-                self._cond.notify()
-        else:
-            self._schedule(delay, fn, *args)
-
     def _after(self, delay: float, fn, *args) -> None:
         """A task's next lifecycle step: due now, it runs right here (an agent drives its own task
         from STARTING to RUNNING to its first check without queueing behind every other task's
@@ -865,7 +853,7 @@ class LocalMaster:
                 self.behavior.launch(self, task, agent)
             else:
                 timing = self.behavior.timing(t)
-                self._next(timing.starting_s, self._lifecycle_starting, task, task.epoch, timing)
+                self._schedule(timing.starting_s, self._lifecycle_starting, task, task.epoch, timing)
 
     # -- task lifecycle ----------------------------------------------------------------
     def _lifecycle_starting(self, task: _Task, epoch: int, timing: TaskTiming) -> None:
