@@ -713,3 +713,43 @@ def test_relaunch_kill_status_revives_instead_of_kicking(drv):
     task_killer.kill_task(P.TaskID(value="t3"), relaunch=True)
     fs.status_update(drv, _status("t3", P.TASK_KILLED))
     assert calls == ["kick", "revive"]
+
+
+def test_reoffer_bypasses_spacing_only_above_the_bucket_floor(drv):
+    """A crash loop that keeps releasing reservations drains the bucket to its floor; from there
+    the re-offer revives keep the slow spacing like any other revive."""
+    from dcos_commons_amd.framework.offer_processing import ReviveManager, TokenBucket
+
+    class Clock:
+        t = 1000.0
+
+        def __call__(self):
+            return self.t
+
+    c = Clock()
+    rm = ReviveManager(TokenBucket(initial=4, capacity=4, acquire_interval_s=5.0, burst_interval_s=1.0, clock=c))
+    revived = 0
+    for _ in range(4):
+        rm.request_revive(bypass_spacing=True)
+        revived += rm.revive_if_requested()
+    # tokens 4 -> 2: the first two revives bypass the 1 s spacing; at the floor (2) they do not
+    assert revived == 2 and rm.revive_requested and drv.revives == 2
+    c.t += 5.0
+    assert rm.revive_if_requested() and drv.revives == 3
+
+
+def test_revive_only_wakeup_schedules_a_fallback_cycle(drv):
+    """After a revive-only wake-up the loop runs a full cycle REOFFER_FALLBACK_CYCLE_S later
+    unless an offer comes first (a kill the master answered with LOST frees nothing)."""
+    from dcos_commons_amd.framework import offer_processing as OP
+
+    c = CountingClient()
+    p = processor(c, hold_s=10.0, event_driven=True).disable_threading()
+    p.start()
+    p.reoffer_released()
+    t0 = time.monotonic()
+    p.process_queued_offers(0.5)
+    assert c.status_calls == 0 and p._fallback_cycle_at is not None
+    assert p._fallback_cycle_at - t0 <= OP.REOFFER_FALLBACK_CYCLE_S + 0.05
+    p.process_queued_offers(0)          # what the loop runs when the fallback time comes
+    assert c.status_calls == 1 and p._fallback_cycle_at is None
