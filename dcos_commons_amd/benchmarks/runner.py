@@ -135,7 +135,7 @@ def _run_distributed(args, rank, world, local_rank, use_gpu, dist):
     def local_runner(task_info, devices):
         return check({})[0]
 
-    runners = [local_runner] + [r.run_check for r in remotes]
+    runners = [local_runner] + [agent_link.RemoteCheckRunner(r) for r in remotes]
     bench = DeployBench(world, profile=args.profile, agent_runners=runners, gpu_devices=list(range(world)),
                         allocation_interval_s=args.allocation_interval, extra_env=_sched_env(args))
     for _ in range(args.warmup):

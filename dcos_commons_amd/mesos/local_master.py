@@ -897,6 +897,17 @@ class LocalMaster:
         trace.instant("check_submit", "master", task=task.info.name)
         runner = self._check_runner(task)
         devices = list(task.gpu_devices)
+        run_async = getattr(runner, "run_async", None)
+        if run_async is not None:
+            # the runner reports back by itself (a remote agent's link): no pool thread blocks on it
+            def done(ok: bool) -> None:
+                self._schedule(0, self._check_result, task, epoch, ok)
+            try:
+                run_async(task.info, devices, done)
+            except Exception:  # noqa: BLE001
+                LOGGER.exception("check of %s raised", task.info.name)
+                self._schedule(0, self._check_result, task, epoch, False)
+            return
 
         def work():
             try:

@@ -78,16 +78,23 @@ class RemoteAgent:
                 break
             with self._lock:
                 fut = self._pending.pop(msg.get("id"), None)
-            if fut is not None:
+            if isinstance(fut, Future):
                 fut.set_result(msg)
-        self.alive = False
+            elif fut is not None:
+                fut(msg)  # an asynchronous request's callback, run on this reader thread
         with self._lock:
+            self.alive = False   # under the lock: a request registered after this fails at once
             pending, self._pending = self._pending, {}
         for f in pending.values():
-            f.set_exception(ConnectionError("agent disconnected"))
+            if isinstance(f, Future):
+                f.set_exception(ConnectionError("agent disconnected"))
+            else:
+                f({"ok": False, "detail": "agent disconnected"})
 
     def request(self, op: str, timeout: Optional[float] = None, **fields) -> dict:
         with self._lock:
+            if not self.alive:
+                raise ConnectionError("agent disconnected")
             self._next += 1
             rid = self._next
             fut: Future = Future()
@@ -95,16 +102,57 @@ class RemoteAgent:
         self.conn.send(dict(fields, op=op, id=rid))
         return fut.result(timeout)
 
+    def request_async(self, op: str, callback: Callable[[dict], None], **fields) -> None:
+        """Sends ``op`` and returns at once; ``callback(reply)`` runs on the link's reader thread
+        (with ``{"ok": False}`` if the agent disconnects first)."""
+        with self._lock:
+            alive = self.alive
+            if alive:
+                self._next += 1
+                rid = self._next
+                self._pending[rid] = callback
+        if not alive:
+            callback({"ok": False, "detail": "agent disconnected"})
+            return
+        try:
+            self.conn.send(dict(fields, op=op, id=rid))
+        except OSError:
+            with self._lock:
+                self._pending.pop(rid, None)
+            callback({"ok": False, "detail": "agent link send failed"})
+
     def run_check(self, task_info, devices: List[int]) -> bool:
         """Check runner for ``LocalMaster``: executes the task's check on this agent's GPU."""
         r = self.request("check", timeout=300, task=task_info.task_id.value, name=task_info.name, devices=devices)
         return bool(r.get("ok"))
+
+    def run_check_async(self, task_info, devices: List[int], done: Callable[[bool], None]) -> None:
+        """``LocalMaster``'s asynchronous check protocol: the request goes out from the master's
+        thread and the reply's callback reports the result from the reader thread, so no worker
+        thread sits blocked on the round trip and the result reaches the master one thread hop
+        sooner."""
+        self.request_async("check", lambda r: done(bool(r.get("ok"))), task=task_info.task_id.value,
+                           name=task_info.name, devices=devices)
+
 
     def shutdown(self) -> None:
         try:
             self.conn.send({"op": "shutdown", "id": 0})
         except OSError:
             pass
+
+
+class RemoteCheckRunner:
+    """A check runner bound to a remote agent: callable (blocking) and with ``run_async``."""
+
+    def __init__(self, agent: "RemoteAgent"):
+        self.agent = agent
+
+    def __call__(self, task_info, devices: List[int]) -> bool:
+        return self.agent.run_check(task_info, devices)
+
+    def run_async(self, task_info, devices: List[int], done: Callable[[bool], None]) -> None:
+        self.agent.run_check_async(task_info, devices, done)
 
 
 class AgentLinkServer:
