@@ -528,12 +528,12 @@ class OfferProcessor:
             self.queue.notify()
 
     def reoffer_released(self) -> None:
-        """A task ended that held reservations the plans reuse in place: a kill issued for a
-        relaunch, or a FINISH/ONCE task whose pod's next step runs on the same resource set. The
-        master offers released resources again at its next allocation; wake the loop for a REVIVE
-        (an allocation now) that is not held to the burst spacing while the bucket is above its
-        floor. The offer that carries them wakes the loop for the relaunch. The revive is taken on
-        the offer thread, like every revive (OfferProcessor.java:300-309)."""
+        """A task ended (finished, failed, killed; a kill issued for a relaunch included) and
+        released reservations the plans reuse in place. The master offers released resources
+        again at its next allocation; wake the loop for a REVIVE (an allocation now) that is not
+        held to the burst spacing while the bucket is above its floor. The offer that carries them
+        wakes the loop for the relaunch. The revive is taken on the offer thread, like every
+        revive (OfferProcessor.java:300-309)."""
         if self.event_driven:
             self._reoffer_requests += 1
             self._wake.set()
