@@ -11,7 +11,9 @@ way it runs on a cluster (``testing.cluster.LocalCluster``, SURVEY §4 system-in
   acknowledgements) and keeps its state in ZooKeeper (jute wire protocol, ``SDK_PERSISTER=zk``);
 * with ``executor="process"`` every task is a real process in an agent sandbox, and the readiness
   check is a real command run by the agent (``--probe-cmd``; on an MI355X box
-  ``native/build/amd-gpu-probe --readiness`` runs the HIP probe on the pod's device).
+  ``native/build/amd-gpu-probe --readiness`` runs the HIP probe on the pod's device, starting a HIP
+  runtime per check; with ``--probe-service`` the node's readiness service ``amd-gpu-probed``
+  keeps one runtime resident and the check is ``native/build/amd-gpu-ready``).
 
 Timing follows BASELINE.md: deploy is measured from the master accepting the framework's SUBSCRIBE
 to ``GET /v1/plans/deploy`` answering 200 (the scheduler process start-up and imports are outside
@@ -106,7 +108,8 @@ def _post(url: str) -> int:
 
 class ClusterBench:
     def __init__(self, agents: int = 1, executor: str = "process", probe_cmd: str = DEFAULT_PROBE,
-                 allocation_interval_s: float = 1.0, timeout_s: float = 120.0, profile_env: Optional[dict] = None):
+                 allocation_interval_s: float = 1.0, timeout_s: float = 120.0, profile_env: Optional[dict] = None,
+                 probe_service: bool = False):
         from dcos_commons_amd.testing.cluster import LocalCluster, use
 
         self.n = agents
@@ -116,7 +119,8 @@ class ClusterBench:
         env.update(profile_env or {})
         # ZooKeeper in its own process, as on a cluster (the master and agents stay in this one)
         self.cluster = LocalCluster(agents=agents, gpus_per_agent=1, executor=executor, zk_process=True,
-                                    allocation_interval_s=allocation_interval_s, scheduler_env=env).start()
+                                    allocation_interval_s=allocation_interval_s, scheduler_env=env,
+                                    gpu_probe_service=probe_service).start()
         use(self.cluster)
         self.watch = _Watch(self.cluster)
         self._seq = 0
@@ -203,14 +207,23 @@ def main(argv: Optional[List[str]] = None) -> int:
     ap.add_argument("--probe-cmd", default=DEFAULT_PROBE, help="the pods' readiness check command")
     ap.add_argument("--profile", choices=sorted(PROFILES), default="mi355x")
     ap.add_argument("--allocation-interval", type=float, default=1.0)
+    ap.add_argument("--probe-service", action="store_true",
+                    help="run the node's GPU readiness service; the default check becomes amd-gpu-ready")
     args = ap.parse_args(argv)
+    if args.probe_service and args.probe_cmd == DEFAULT_PROBE:
+        from dcos_commons_amd.ops.probe_service import CLIENT_BINARY
+
+        args.probe_cmd = CLIENT_BINARY
     logging.basicConfig(level=logging.ERROR)
     bench = ClusterBench(args.agents, args.executor, args.probe_cmd, args.allocation_interval,
-                         profile_env=PROFILES[args.profile])
+                         profile_env=PROFILES[args.profile], probe_service=args.probe_service)
+    served = None
     try:
         for _ in range(args.warmup):
             bench.run_cycle()
         cycles = [bench.run_cycle() for _ in range(args.cycles)]
+        if bench.cluster.probe_service is not None:
+            served = bench.cluster.probe_service.served()
     finally:
         bench.close()
 
@@ -220,7 +233,8 @@ def main(argv: Optional[List[str]] = None) -> int:
 
     print(json.dumps({"bench": "cluster", "agents": args.agents, "pods": args.agents, "cycles": args.cycles,
                       "executor": args.executor, "probe_cmd": args.probe_cmd, "profile": args.profile,
-                      "allocation_interval_s": args.allocation_interval,
+                      "allocation_interval_s": args.allocation_interval, "probe_service": args.probe_service,
+                      "probe_service_checks": served,
                       "deploy_s": stat("deploy_s"), "mttr_restart_s": stat("mttr_restart_s"),
                       "mttr_replace_s": stat("mttr_replace_s"),
                       "data": "scheduler process + v1 HTTP API + ZooKeeper; helloworld gpu.yml, gpus:1 per pod"}),

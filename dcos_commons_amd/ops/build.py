@@ -2,6 +2,8 @@
 
 * ``dcos_commons_amd/ops/_amdprobe.so`` -- HIP probe kernels (C ABI, loaded with ctypes);
 * ``native/build/amd-gpu-probe``       -- standalone HIP probe binary (readiness check command);
+* ``native/build/amd-gpu-probed``      -- node-local readiness service (keeps the HIP runtime and the
+  per-device probe contexts resident; ``amd-gpu-ready``, a CMake target, is its client);
 * ``native/build/sdk-bootstrap``, ``native/build/sdk-cli`` -- C++ task bootstrap and service CLI.
 
 Everything is compiled directly with ``hipcc --offload-arch=gfx950`` / ``g++`` (no hipify, no
@@ -64,6 +66,16 @@ def build_probe_binary(force: bool = False, verbose: bool = False) -> str:
     return out
 
 
+def build_probe_service(force: bool = False, verbose: bool = False) -> str:
+    os.makedirs(BUILD, exist_ok=True)
+    out = os.path.join(BUILD, "amd-gpu-probed")
+    srcs = [os.path.join(NATIVE, "probe", "probed.cpp"), os.path.join(OPS, "csrc", "probe_api.hip")]
+    deps = srcs + [os.path.join(OPS, "csrc", "probe_kernels.hip")]
+    if force or _stale(out, deps):
+        _run([hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-pthread", *srcs, "-o", out], verbose)
+    return out
+
+
 def build_cpp_tools(force: bool = False, verbose: bool = False, sanitize: bool = False) -> List[str]:
     """CMake build of the C++ natives (bootstrap, CLI, TLS crypto library) if their sources exist.
 
@@ -73,7 +85,8 @@ def build_cpp_tools(force: bool = False, verbose: bool = False, sanitize: bool =
         return []
     out = BUILD_SANITIZE if sanitize else BUILD
     os.makedirs(out, exist_ok=True)
-    names = ("sdk-bootstrap", "sdk-cli", "native-tests", "tls-tests") + (() if sanitize else ("libsdktls.so",))
+    names = ("sdk-bootstrap", "sdk-cli", "native-tests", "tls-tests", "amd-gpu-ready") + (
+        () if sanitize else ("libsdktls.so",))
     targets = [os.path.join(out, n) for n in names]
     srcs = []
     for d, _, fs in os.walk(NATIVE):
@@ -95,6 +108,8 @@ def build_all(force: bool = False, verbose: bool = False) -> List[str]:
     out = [build_probe_lib(force, verbose)]
     if os.path.exists(os.path.join(NATIVE, "probe", "amd_gpu_probe.hip")):
         out.append(build_probe_binary(force, verbose))
+    if os.path.exists(os.path.join(NATIVE, "probe", "probed.cpp")):
+        out.append(build_probe_service(force, verbose))
     out.extend(build_cpp_tools(force, verbose))
     return out
 

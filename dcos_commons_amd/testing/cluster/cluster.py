@@ -148,7 +148,8 @@ class LocalCluster:
                  agent_cpus: float = 8.0, agent_mem: float = 32768.0, agent_disk: float = 65536.0,
                  packages: Optional[Dict[str, str]] = None, scheduler_env: Optional[Dict[str, str]] = None,
                  finish_tasks: Sequence[str] = (), dcos_version: str = "1.13.0", keep_work_dir: bool = False,
-                 mount_disks: Sequence[tuple] = (), dcos_security: bool = False, zk_process: bool = False):
+                 mount_disks: Sequence[tuple] = (), dcos_security: bool = False, zk_process: bool = False,
+                 gpu_probe_service: bool = False):
         self.work_dir = os.path.abspath(work_dir or tempfile.mkdtemp(prefix="sdk-cluster-"))
         self._own_work_dir = work_dir is None and not keep_work_dir
         self.region = region
@@ -202,6 +203,12 @@ class LocalCluster:
         self.agent_ids: Dict[str, str] = {}  # hostname -> agent id
         self.zk = None  # ZkServer, or a _ZkProcess with zk_process=True
         self.zk_process = zk_process
+        # the node's GPU readiness service (ops.probe_service): tasks find it through
+        # AMD_GPU_PROBE_SOCKET, and `amd-gpu-ready` checks run against the resident HIP runtime
+        if gpu_probe_service and executor != "process":
+            raise ValueError("gpu_probe_service needs executor='process' (the checks are task commands)")
+        self.gpu_probe_service = gpu_probe_service
+        self.probe_service = None
         self.http_master: Optional[HttpMaster] = None
         self.marathon = LocalMarathon(self)
         from dcos_commons_amd.testing.cluster.metronome import LocalMetronome
@@ -212,13 +219,22 @@ class LocalCluster:
 
     # -- lifecycle -------------------------------------------------------------------------
     def start(self) -> "LocalCluster":
-        if self.dcos is not None:
-            self.dcos.start()
-        self.zk = _ZkProcess().start() if self.zk_process else ZkServer().start()
-        self.http_master = HttpMaster(self.master).start()
-        for spec in self._agent_specs:
-            self.agent_ids[spec.hostname] = self.master.add_agent(spec)
-        self._started = True
+        self._started = True   # a start that fails part-way is shut down: no ZooKeeper process left behind
+        try:
+            if self.dcos is not None:
+                self.dcos.start()
+            self.zk = _ZkProcess().start() if self.zk_process else ZkServer().start()
+            if self.gpu_probe_service:
+                from dcos_commons_amd.ops.probe_service import ProbeService
+
+                self.probe_service = ProbeService(os.path.join(self.work_dir, "gpu-probe.sock")).start()
+                self.behavior.extra_env.update(self.probe_service.task_env)
+            self.http_master = HttpMaster(self.master).start()
+            for spec in self._agent_specs:
+                self.agent_ids[spec.hostname] = self.master.add_agent(spec)
+        except BaseException:
+            self.shutdown()
+            raise
         return self
 
     def shutdown(self) -> None:
@@ -230,6 +246,8 @@ class LocalCluster:
         if self.http_master is not None:
             self.http_master.stop()
         self.master.shutdown()
+        if self.probe_service is not None:
+            self.probe_service.stop()
         if self.zk is not None:
             self.zk.stop()
         if self.dcos is not None:
