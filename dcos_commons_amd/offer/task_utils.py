@@ -124,8 +124,9 @@ def are_different(old: TaskSpec, new: TaskSpec) -> bool:
     return False
 
 
-def get_pod_spec(service_spec: ServiceSpec, task_info: P.TaskInfo) -> Optional[PodSpec]:
-    pod_type = TaskLabelReader(task_info).get_type()
+def get_pod_spec(service_spec: ServiceSpec, task_info: P.TaskInfo,
+                 reader: Optional[TaskLabelReader] = None) -> Optional[PodSpec]:
+    pod_type = (reader or TaskLabelReader(task_info)).get_type()
     return service_spec.pod(pod_type)
 
 
@@ -148,23 +149,25 @@ def get_goal_state(pod_instance: PodInstance, task_name: str) -> GoalState:
     return spec.goal
 
 
-def get_pod_instance(config_store, task_info: P.TaskInfo) -> PodInstance:
-    """Resolve a TaskInfo to its PodInstance using the config it was launched with."""
-    reader = TaskLabelReader(task_info)
+def get_pod_instance(config_store, task_info: P.TaskInfo, reader: Optional[TaskLabelReader] = None) -> PodInstance:
+    """Resolve a TaskInfo to its PodInstance using the config it was launched with (``reader``:
+    the task's label reader, when the caller already has one)."""
+    reader = reader or TaskLabelReader(task_info)
     config_id = reader.get_target_configuration()
     try:
         service_spec = config_store.fetch(config_id)
     except Exception as e:  # noqa: BLE001
         raise TaskException(
             f"Unable to retrieve ServiceSpecification ID {config_id} referenced by TaskInfo[{task_info.name}]") from e
-    pod = get_pod_spec(service_spec, task_info)
+    pod = get_pod_spec(service_spec, task_info, reader)
     if pod is None:
         raise TaskException(f"No TaskSpecification found for TaskInfo[{task_info.name}]")
     return PodInstance(pod, reader.get_index())
 
 
-def get_task_spec_for_info(config_store, task_info: P.TaskInfo) -> Optional[TaskSpec]:
-    return get_task_spec(get_pod_instance(config_store, task_info), task_info.name)
+def get_task_spec_for_info(config_store, task_info: P.TaskInfo,
+                           reader: Optional[TaskLabelReader] = None) -> Optional[TaskSpec]:
+    return get_task_spec(get_pod_instance(config_store, task_info, reader), task_info.name)
 
 
 def is_eligible_for_recovery(task_spec: TaskSpec) -> bool:
@@ -186,10 +189,11 @@ def get_tasks_needing_recovery(config_store, all_task_infos, all_statuses) -> Li
         status = status_map.get(info.task_id.value)
         if status is None:
             continue
-        spec = get_task_spec_for_info(config_store, info)
+        reader = TaskLabelReader(info)   # one label map per task for the spec lookup and the failed mark
+        spec = get_task_spec_for_info(config_store, info, reader)
         if spec is None:
             raise TaskException(f"Failed to determine TaskSpec from TaskInfo: {info.name}")
-        if is_eligible_for_recovery(spec) and (is_recovery_needed(status) or is_permanently_failed(info)):
+        if is_eligible_for_recovery(spec) and (is_recovery_needed(status) or reader.is_permanently_failed()):
             out.append(info)
     return out
 

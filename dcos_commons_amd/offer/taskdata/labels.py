@@ -9,6 +9,7 @@ rest of the scheduler -- and the checkpointed state -- relies on.
 from __future__ import annotations
 
 import base64
+import functools
 import re
 import uuid
 from typing import Dict, List, Optional
@@ -155,6 +156,13 @@ def scalar_attribute(name: str, value: float) -> P.Attribute:
 # task labels
 
 
+@functools.lru_cache(maxsize=256)
+def _config_uuid(text: str) -> uuid.UUID:
+    """UUIDs are immutable and a service has a handful of config IDs: every task's label parses to
+    one of them, on every recovery-plan pass."""
+    return uuid.UUID(text)
+
+
 class TaskLabelReader:
     def __init__(self, task_info: P.TaskInfo):
         self._name = task_info.name
@@ -186,7 +194,7 @@ class TaskLabelReader:
         return self._get_or_throw(OFFER_HOSTNAME_LABEL)
 
     def get_target_configuration(self) -> uuid.UUID:
-        return uuid.UUID(self._get_or_throw(TARGET_CONFIGURATION_LABEL))
+        return _config_uuid(self._get_or_throw(TARGET_CONFIGURATION_LABEL))
 
     def get_gpu_devices(self) -> List[int]:
         v = self._labels.get(GPU_DEVICES_LABEL)

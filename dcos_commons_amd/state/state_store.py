@@ -226,16 +226,19 @@ class StateStore:
         return t
 
     def fetch_statuses(self) -> List[P.TaskStatus]:
+        """Every stored TaskStatus, read in one persister call (tasks without one are skipped)."""
+        paths = [self._task_status_path(n) for n in self.fetch_task_names()]
+        try:
+            raw = self.persister.get_many(paths)
+        except PersisterException as e:
+            raise StateStoreException(e.reason, str(e)) from e
         out = []
-        for name in self.fetch_task_names():
-            try:
-                data = self.persister.get(self._task_status_path(name))
-            except PersisterException as e:
-                if e.reason == Reason.NOT_FOUND:
-                    continue
-                raise StateStoreException(e.reason, str(e)) from e
+        for path in paths:
+            data = raw.get(path)
+            if data is None:
+                continue
             s = P.TaskStatus()
-            s.ParseFromString(data or b"")
+            s.ParseFromString(data)
             out.append(s)
         return out
 
