@@ -758,26 +758,44 @@ class LocalMaster:
             return list(op.launch.task_infos)
         return []
 
+    @staticmethod
+    def _swap_in_place(bag: ResourceBag, pairs) -> None:
+        """For each ``(take, give)``: subtract ``take`` from ``bag``, then add ``give``. All or
+        nothing: on a shortfall the pairs already applied are undone before the error propagates
+        (the result is what applying them to a copy and keeping it on success gives, without
+        copying the offer's whole bag for every operation)."""
+        done = []
+        try:
+            for take, give in pairs:
+                bag.subtract(take)
+                done.append((take, None))
+                bag.add(give)
+                done[-1] = (take, give)
+        except InsufficientResources:
+            for take, give in reversed(done):
+                if give is not None:
+                    bag.subtract(give)
+                bag.add(take)
+            raise
+
     def _apply(self, fw: _Framework, agent: _Agent, bag: ResourceBag, op: P.Offer.Operation) -> None:
         T = P.Offer.Operation
         if op.type == T.RESERVE:
-            trial = bag.copy()
+            pairs = []
             for r in op.reserve.resources:
-                trial.subtract(pop_reservation(r))
                 c = P.Resource()
                 c.CopyFrom(r)
                 c.ClearField("allocation_info")
-                trial.add(c)
-            bag._q, bag._proto = trial._q, trial._proto
+                pairs.append((pop_reservation(r), c))
+            self._swap_in_place(bag, pairs)
         elif op.type == T.UNRESERVE:
-            trial = bag.copy()
+            pairs = []
             for r in op.unreserve.resources:
                 c = P.Resource()
                 c.CopyFrom(r)
                 c.ClearField("allocation_info")
-                trial.subtract(c)
-                trial.add(pop_reservation(c))
-            bag._q, bag._proto = trial._q, trial._proto
+                pairs.append((c, pop_reservation(c)))
+            self._swap_in_place(bag, pairs)
         elif op.type == T.CREATE:
             trial = bag.copy()
             for v in op.create.volumes:

@@ -109,11 +109,13 @@ class ResourceBag:
         k = identity(r)
         cur = self._q.get(k)
         q = _quantity(r)
-        if cur is None or not self.contains(r):
-            raise InsufficientResources(f"{r.name} {q} not available (have {cur})")
         if isinstance(q, float):
+            if cur is None or cur + EPS < q:
+                raise InsufficientResources(f"{r.name} {q} not available (have {cur})")
             nv = round((cur - q) * 1000.0) / 1000.0
         else:
+            if cur is None or subtract_intervals(q, cur) != []:
+                raise InsufficientResources(f"{r.name} {q} not available (have {cur})")
             nv = subtract_intervals(cur, q)
         if _is_empty(nv):
             del self._q[k]
