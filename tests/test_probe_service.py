@@ -265,3 +265,24 @@ def test_cluster_gpu_pod_goes_ready_through_the_service():
     finally:
         bench.close()
     assert r["deploy_s"] < 10 and r["mttr_restart_s"] < 10 and r["mttr_replace_s"] < 10, r
+
+
+def test_cluster_probe_service_needs_process_executor():
+    from dcos_commons_amd.testing.cluster import LocalCluster
+
+    with pytest.raises(ValueError):
+        LocalCluster(agents=1, executor="synthetic", gpu_probe_service=True)
+
+
+@pytest.mark.skipif(_has_gpu(), reason="needs a host where the service cannot start")
+def test_cluster_start_failure_shuts_down_what_started(daemon_binary):
+    """The service cannot start without a GPU: start() raises and leaves no ZooKeeper, master or
+    work directory behind."""
+    from dcos_commons_amd.testing.cluster import LocalCluster
+
+    c = LocalCluster(agents=1, gpus_per_agent=1, gpu_probe_service=True, zk_process=True)
+    with pytest.raises(RuntimeError, match="GPU probe service did not start"):
+        c.start()
+    assert c.zk.proc.poll() is not None                       # the ZooKeeper process was stopped
+    assert not os.path.exists(c.work_dir)
+    assert not c.master._thread.is_alive()
