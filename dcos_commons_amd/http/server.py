@@ -10,11 +10,11 @@ from __future__ import annotations
 import logging
 import socket
 import threading
-import socketserver
-from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
+from http.server import BaseHTTPRequestHandler
 from typing import Callable, Iterable, Optional
 
 from dcos_commons_amd.framework.process_exit import ProcessExit
+from dcos_commons_amd.utils.http_server import QuietThreadingHTTPServer
 
 from .api import Router
 from .resources import MetricsResource
@@ -71,24 +71,11 @@ class _Handler(BaseHTTPRequestHandler):
         self._handle("DELETE")
 
 
-class _HttpServer(ThreadingHTTPServer):
-    """``ThreadingHTTPServer`` without the reverse DNS lookup ``HTTPServer.server_bind`` does
-    (``socket.getfqdn`` of the bind address) only to fill ``server_name``, which nothing here
-    reads: the lookup sits on the scheduler's start-up path, and on a host whose resolver goes
-    to the network it is the slowest step of it."""
-
-    def server_bind(self):
-        socketserver.TCPServer.server_bind(self)
-        host, port = self.server_address[:2]
-        self.server_name = host
-        self.server_port = port
-
-
 class ApiServer:
     def __init__(self, port: int, resources: Iterable, host: str = "127.0.0.1"):
         self.router = Router(list(resources) + [MetricsResource()])
         handler = type("Handler", (_Handler,), {"router": self.router})
-        self.httpd = _HttpServer((host, port), handler)
+        self.httpd = QuietThreadingHTTPServer((host, port), handler)
         self.httpd.daemon_threads = True
         self.port = self.httpd.server_address[1]
         self._thread: Optional[threading.Thread] = None

@@ -399,12 +399,30 @@ class ProcessTaskBehavior(TaskBehavior):
                 pass
         return n
 
+    @staticmethod
+    def _signal_group(proc: _Proc, sig: int) -> None:
+        """The task's process group (its session leader's group: ``bash -c`` and whatever it runs
+        without job control), in one ``killpg`` instead of a ``/proc`` scan."""
+        if proc.popen is None:
+            return
+        try:
+            os.killpg(proc.popen.pid, sig)
+        except (ProcessLookupError, PermissionError):
+            pass
+
     def _terminate(self, proc: _Proc, grace_s: float) -> None:
+        """SIGTERM now to the task's process group, from the caller's thread (the master's, on a
+        KILL); then, off that thread, SIGTERM to anything else left in the task's session (a
+        child that made its own process group), and SIGKILL to the whole session after the grace
+        period. Scanning ``/proc`` for the session costs ~10 ms of interpreter time on a busy host,
+        which the kill used to spend before the master could go on."""
         proc.health_stop.set()
-        self._signal_session(proc, signal.SIGTERM)
+        self._signal_group(proc, signal.SIGTERM)
 
         def escalate():
+            self._signal_session(proc, signal.SIGTERM)
             if not proc.exited.wait(max(0.0, grace_s)):
+                self._signal_group(proc, signal.SIGKILL)
                 self._signal_session(proc, signal.SIGKILL)
         threading.Thread(target=escalate, name=f"kill-{proc.name}", daemon=True).start()
 

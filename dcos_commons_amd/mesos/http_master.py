@@ -24,7 +24,7 @@ import sys
 import threading
 import time
 import uuid
-from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
+from http.server import BaseHTTPRequestHandler
 from typing import Dict, List, Optional
 
 from dcos_commons_amd.mesos import protos as P
@@ -32,6 +32,7 @@ from dcos_commons_amd.mesos import recordio
 from dcos_commons_amd.mesos.http_driver import JSON, PROTOBUF, SCHEDULER_PATH, STREAM_ID_HEADER, decode_message, \
     encode_message
 from dcos_commons_amd.mesos.local_master import AgentSpec, LocalMaster, TERMINAL
+from dcos_commons_amd.utils.http_server import QuietThreadingHTTPServer
 
 LOGGER = logging.getLogger(__name__)
 _CLOSE = object()
@@ -113,7 +114,7 @@ class HttpMaster:
         class Handler(_Handler):
             owner = facade
 
-        self.httpd = ThreadingHTTPServer((host, port), Handler)
+        self.httpd = QuietThreadingHTTPServer((host, port), Handler)
         self.httpd.daemon_threads = True
         self._thread: Optional[threading.Thread] = None
 

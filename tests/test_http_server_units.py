@@ -1,0 +1,43 @@
+"""``utils.http_server.QuietThreadingHTTPServer``, the server behind the scheduler API and the
+Mesos master stand-in: no reverse DNS lookup at bind, client disconnects logged quietly."""
+import logging
+import socket
+import threading
+import time
+import urllib.request
+from http.server import BaseHTTPRequestHandler
+
+from dcos_commons_amd.utils.http_server import QuietThreadingHTTPServer
+
+
+def test_quiet_http_server_drops_client_disconnects_only(caplog):
+    """The API/master HTTP server: a client that went away is a debug line, not a traceback on
+    stderr; any other handler error is still logged as an error."""
+    class H(BaseHTTPRequestHandler):
+        def do_GET(self):
+            if self.path == "/gone":
+                raise BrokenPipeError("client went away")
+            raise ValueError("handler bug")
+
+        def log_message(self, *a):
+            pass
+
+    srv = QuietThreadingHTTPServer(("127.0.0.1", 0), H)
+    assert srv.server_name == "127.0.0.1"               # no reverse lookup of the bind address
+    t = threading.Thread(target=srv.serve_forever, kwargs={"poll_interval": 0.05}, daemon=True)
+    t.start()
+    try:
+        with caplog.at_level(logging.DEBUG, logger="dcos_commons_amd.utils.http_server"):
+            for path in ("/gone", "/bug"):
+                try:
+                    urllib.request.urlopen(f"http://127.0.0.1:{srv.server_address[1]}{path}", timeout=5)
+                except (OSError, socket.error):
+                    pass
+            deadline = time.monotonic() + 5
+            while len(caplog.records) < 2 and time.monotonic() < deadline:
+                time.sleep(0.01)
+        levels = sorted((r.levelname, r.getMessage().split(":")[0]) for r in caplog.records)
+        assert [lv for lv, _ in levels] == ["DEBUG", "ERROR"], levels
+    finally:
+        srv.shutdown()
+        srv.server_close()

@@ -62,3 +62,4 @@ def test_reserve_operation_is_all_or_nothing():
     with pytest.raises(InsufficientResources):
         LocalMaster._swap_in_place(bag, back)
     assert _state(bag) == snapshot
+
