@@ -118,9 +118,7 @@ class FrameworkRunner:
         self.driver = factory(self.framework_scheduler, info)
         if not block:
             self.driver.start()
-            self.framework_scheduler.prestart()   # overlaps the SUBSCRIBE round trip
             return self.driver
-        self.framework_scheduler.prestart()
         self.driver.run()
         self.api_server.join()
         ProcessExit.exit(ProcessExit.DRIVER_EXITED)

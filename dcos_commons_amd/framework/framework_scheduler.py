@@ -212,11 +212,6 @@ class FrameworkScheduler:
         LOGGER.error("SchedulerDriver returned an error, shutting down: %s", message)
         ProcessExit.exit(ProcessExit.ERROR)
 
-    def prestart(self) -> None:
-        """The background threads ``registered`` starts, created ahead and parked until then."""
-        self.offer_processor.prestart()
-        self.implicit_reconciler.prestart()
-
     def stop(self) -> None:
         self.offer_processor.stop()
         self.implicit_reconciler.stop()

@@ -479,7 +479,6 @@ class OfferProcessor:
         # brings one sooner (a kill of a task the master did not know frees nothing to re-offer)
         self._fallback_cycle_at: Optional[float] = None
         self._stop = threading.Event()
-        self._go = threading.Event()   # start() (or stop()) releases a prestarted loop
         self._thread: Optional[threading.Thread] = None
         self.cycles = 0
 
@@ -491,28 +490,20 @@ class OfferProcessor:
         self.revive_manager.bucket = bucket
         return self
 
-    def prestart(self) -> None:
-        """Create the offer thread ahead of registration, parked until ``start()``: the thread
-        start handshake then overlaps the SUBSCRIBE round trip instead of following it."""
+    def start(self) -> None:
         if self.multithreaded and self._thread is None:
             self._thread = threading.Thread(target=self._loop, name="OfferProcessor", daemon=True)
             self._thread.start()
-
-    def start(self) -> None:
-        self.prestart()
         self._initialized = True
-        self._go.set()
 
     def stop(self) -> None:
         self._stop.set()
-        self._go.set()
         self._wake.set()
         self.queue.notify()
         if self._thread is not None:
             self._thread.join(timeout=5)
 
     def _loop(self) -> None:
-        self._go.wait()
         while not self._stop.is_set():
             try:
                 wait = self.offer_wait_s
@@ -801,7 +792,6 @@ class ImplicitReconciler:
         self.multithreaded = True
         self.started = False
         self._stop = threading.Event()
-        self._go = threading.Event()   # start() (or stop()) releases a prestarted thread
         self._thread = None
 
     def disable_threading(self) -> "ImplicitReconciler":
@@ -817,14 +807,15 @@ class ImplicitReconciler:
         except Exception:  # noqa: BLE001
             LOGGER.exception("Failed to trigger implicit reconciliation")
 
-    def prestart(self) -> None:
-        """Create the thread ahead of registration, parked until ``start()`` (see
-        ``OfferProcessor.prestart``)."""
-        if not self.multithreaded or self._thread is not None:
+    def start(self) -> None:
+        if self.started:
+            raise RuntimeError("Start was already called")
+        self.started = True
+        if not self.multithreaded:
+            self._reconcile()
             return
 
         def loop():
-            self._go.wait()
             if self._stop.wait(self.delay_s):
                 return
             while True:
@@ -835,17 +826,6 @@ class ImplicitReconciler:
         self._thread = threading.Thread(target=loop, name="ImplicitReconciler", daemon=True)
         self._thread.start()
 
-    def start(self) -> None:
-        if self.started:
-            raise RuntimeError("Start was already called")
-        self.started = True
-        if not self.multithreaded:
-            self._reconcile()
-            return
-        self.prestart()
-        self._go.set()
-
     def stop(self) -> None:
         self._stop.set()
-        self._go.set()
         self.started = False
