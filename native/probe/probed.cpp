@@ -46,6 +46,7 @@ extern "C" int amdprobe_readiness(int device, unsigned seed, int inject, double*
 namespace {
 
 constexpr double MAX_GEMM_REL_ERR = 1e-3;  // ops/gpu_health.py MAX_GEMM_REL_ERR
+constexpr int MAX_INFLIGHT = 64;           // concurrent requests served (one thread each)
 std::atomic<bool> g_stop{false};
 std::atomic<int> g_inflight{0};
 std::atomic<long long> g_last_request_ms{0};
@@ -214,7 +215,12 @@ int main(int argc, char** argv) {
     if (r < 0 && errno != EINTR) break;
     if (r > 0 && (pfd.revents & POLLIN)) {
       const int cfd = ::accept4(lfd, nullptr, nullptr, SOCK_CLOEXEC);
-      if (cfd >= 0) {
+      if (cfd >= 0 && g_inflight.load() >= MAX_INFLIGHT) {
+        // more concurrent checks than a node has GPUs many times over: refuse rather than spawn
+        // without bound (the check fails and the agent retries it at its next interval)
+        write_all(cfd, "{\"error\": \"busy\"}\n");
+        ::close(cfd);
+      } else if (cfd >= 0) {
         g_inflight.fetch_add(1);
         g_last_request_ms.store(now_ms());
         std::thread(serve_connection, cfd).detach();
