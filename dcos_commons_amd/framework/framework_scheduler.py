@@ -180,8 +180,13 @@ class FrameworkScheduler:
             # carries the stale reservations to release, which a scheduler that has gone idle
             # (suppressed) would otherwise never be offered.
             released = status.state in _RELEASING_STATES and resp.result != TaskStatusResult.UNKNOWN_TASK
-            if resp.result == TaskStatusResult.UNKNOWN_TASK or reconciling or \
-                    (can_create_work(status) and not relaunch_kill):
+            work = can_create_work(status) and not relaunch_kill
+            if work and status.state == P.TASK_RUNNING:
+                # a readiness result: does any plan have a step it could unblock, or is this the
+                # end of the last launched step (the cycle then suppresses offers)?
+                useful = getattr(self.client, "offer_cycle_useful", None)
+                work = useful is None or useful()
+            if resp.result == TaskStatusResult.UNKNOWN_TASK or reconciling or work:
                 self.offer_processor.kick()
             if relaunch_kill or released:
                 self.offer_processor.reoffer_released()

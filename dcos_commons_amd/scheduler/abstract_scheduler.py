@@ -19,6 +19,7 @@ from dcos_commons_amd.scheduler.mesos_event_client import (
     OfferResponse,
     TaskStatusResponse,
 )
+from dcos_commons_amd.scheduler.plan.status import Status
 from dcos_commons_amd.scheduler.reconciliation import ExplicitReconciler, LaunchWatchdog, WorkSetTracker
 from dcos_commons_amd.state.state_store import StateStoreException
 from dcos_commons_amd.storage.persister import Reason
@@ -82,6 +83,27 @@ class AbstractScheduler(MesosEventClient):
                     if step.is_running():
                         out.append(step)
         return out
+
+    def offer_cycle_useful(self) -> bool:
+        """After a RUNNING status (readiness passed, or no check): whether an offer cycle could
+        find anything to do. False only while every incomplete step of every plan is launched and
+        waiting (STARTING/STARTED): no step can become a candidate until one of them completes or
+        fails (a failure is a terminal status, which always wakes the offer loop), and the
+        scheduler is not idle, so there is nothing to suppress either. An 8-pod parallel deploy
+        otherwise runs an empty cycle after each of the first seven readiness results, holding the
+        interpreter the next result needs."""
+        in_flight = False
+        for pm in self.plan_coordinator.get_plan_managers():
+            for phase in pm.get_plan().get_children():
+                for step in phase.get_children():
+                    st = step.get_status()
+                    if st == Status.COMPLETE:
+                        continue
+                    if st in (Status.STARTING, Status.STARTED):
+                        in_flight = True
+                        continue
+                    return True
+        return not in_flight
 
     def get_client_status(self):
         self.candidate_steps = list(self.plan_coordinator.get_candidates())

@@ -753,3 +753,91 @@ def test_revive_only_wakeup_schedules_a_fallback_cycle(drv):
     assert p._fallback_cycle_at - t0 <= OP.REOFFER_FALLBACK_CYCLE_S + 0.05
     p.process_queued_offers(0)          # what the loop runs when the fallback time comes
     assert c.status_calls == 1 and p._fallback_cycle_at is None
+
+
+def test_readiness_result_kicks_only_when_a_cycle_can_do_something(drv):
+    """A RUNNING status with its readiness result asks the client whether an offer cycle could
+    find work; other states keep their routing (a terminal status always wakes the loop)."""
+    from dcos_commons_amd.framework.framework_scheduler import FrameworkScheduler
+    from dcos_commons_amd.scheduler.mesos_event_client import TaskStatusResponse
+
+    calls = []
+
+    class OP:
+        def kick(self):
+            calls.append("kick")
+
+        def reoffer_released(self):
+            calls.append("revive")
+
+    class C:
+        useful = False
+
+        def task_status(self, status):
+            return TaskStatusResponse.processed()
+
+        def offer_cycle_useful(self):
+            return self.useful
+
+    def ready(tid):
+        s = _status(tid, P.TASK_RUNNING)
+        s.check_status.type = P.CheckInfo.COMMAND
+        s.check_status.command.exit_code = 0
+        return s
+
+    fs = FrameworkScheduler.__new__(FrameworkScheduler)
+    fs.client, fs.offer_processor = C(), OP()
+    fs.status_update(drv, ready("a"))
+    assert calls == []                                  # other launched steps still pending
+    fs.client.useful = True
+    fs.status_update(drv, ready("b"))
+    assert calls == ["kick"]
+    calls.clear()
+    fs.client.useful = False
+    fs.status_update(drv, _status("c", P.TASK_FAILED))   # a failure always wakes the loop
+    assert calls == ["kick", "revive"]
+
+
+def test_offer_cycle_useful_follows_the_plans():
+    """False only while every incomplete step is launched and waiting for its task."""
+    from dcos_commons_amd.scheduler.abstract_scheduler import AbstractScheduler
+    from dcos_commons_amd.scheduler.plan.status import Status
+
+    class Step:
+        def __init__(self, st):
+            self.st = st
+
+        def get_status(self):
+            return self.st
+
+    class Node:
+        def __init__(self, children):
+            self.children = children
+
+        def get_children(self):
+            return self.children
+
+    class PM:
+        def __init__(self, *statuses):
+            self.plan = Node([Node([Step(s) for s in statuses])])
+
+        def get_plan(self):
+            return self.plan
+
+    class Coord:
+        def __init__(self, *pms):
+            self.pms = pms
+
+        def get_plan_managers(self):
+            return list(self.pms)
+
+    def useful(*pms):
+        s = AbstractScheduler.__new__(AbstractScheduler)
+        s.plan_coordinator = Coord(*pms)
+        return s.offer_cycle_useful()
+
+    assert not useful(PM(Status.COMPLETE, Status.STARTED, Status.STARTING), PM())
+    assert useful(PM(Status.COMPLETE, Status.STARTED, Status.PENDING))        # a step to launch
+    assert useful(PM(Status.STARTED), PM(Status.WAITING))                     # e.g. held back by a conflict
+    assert useful(PM(Status.COMPLETE, Status.COMPLETE), PM())                 # all done: time to suppress
+    assert useful(PM(Status.STARTED, Status.DELAYED))
