@@ -50,10 +50,11 @@ PROFILES = {
 
 @dataclass
 class CycleResult:
-    deploy_s: float
+    deploy_s: float            # from the scheduler's construction (SchedulerRunner.run) to deploy COMPLETE
     mttr_restart_s: float
     mttr_replace_s: float
     total_s: float
+    deploy_from_subscribed_s: float = 0.0   # BASELINE.md protocol: from SUBSCRIBED to deploy COMPLETE
 
 
 def helloworld_env(n_pods: int, gpus_per_pod: int, probe_cmd: str) -> Dict[str, str]:
@@ -155,7 +156,19 @@ class DeployBench:
         spec = ServiceSpecGenerator(raw, cfg, SPECS, env).build()
         master = self._make_master()
         builder = SchedulerBuilder(spec, cfg, MemPersister()).set_plans_from(raw)
-        runner = SchedulerRunner(builder, driver_factory=lambda s, info: LocalSchedulerDriver(master, s, info))
+        marks = {}
+
+        def driver_factory(sched, info):
+            # SUBSCRIBED reaches the scheduler as its `registered` callback: the start of the
+            # BASELINE.md deploy window (the scheduler's construction and API server come before)
+            orig = sched.registered
+
+            def registered(*a, **k):
+                marks.setdefault("subscribed", time.perf_counter())
+                return orig(*a, **k)
+            sched.registered = registered
+            return LocalSchedulerDriver(master, sched, info)
+        runner = SchedulerRunner(builder, driver_factory=driver_factory)
         try:
             t0 = time.perf_counter()
             runner.run(block=False)
@@ -164,7 +177,9 @@ class DeployBench:
             sched = runner.scheduler
             ev = sched.status_processed
             self._wait(lambda: self._plan_done(sched, "deploy"), "deploy plan COMPLETE", ev)
-            deploy_s = time.perf_counter() - t0
+            t_done = time.perf_counter()
+            deploy_s = t_done - t0
+            deploy_sub = t_done - marks.get("subscribed", t0)
             self._expect_api(router, "deploy")
 
             # failures are injected in steady state: deploy finished and the offer loop has gone
@@ -196,4 +211,4 @@ class DeployBench:
         finally:
             runner.stop()
             master.shutdown()
-        return CycleResult(deploy_s, mttr_restart, mttr_replace, time.perf_counter() - t_cycle)
+        return CycleResult(deploy_s, mttr_restart, mttr_replace, time.perf_counter() - t_cycle, deploy_sub)
