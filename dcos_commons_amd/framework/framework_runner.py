@@ -13,6 +13,7 @@ rules.
 """
 from __future__ import annotations
 
+import gc
 import logging
 import os
 import sys
@@ -97,6 +98,10 @@ class FrameworkRunner:
         switch_s = self.scheduler_config.gil_switch_interval_s()
         if switch_s > 0:
             sys.setswitchinterval(switch_s)
+        gen0 = self.scheduler_config.gc_gen0_threshold()
+        if gen0 > 0:
+            _, g1, g2 = gc.get_threshold()
+            gc.set_threshold(gen0, g1, g2)
         cpus = self.scheduler_config.cpu_set()
         if cpus:
             try:

@@ -268,6 +268,13 @@ class SchedulerConfig:
         22-37 ms outliers against <= 16 ms at 5 ms, profiles/ab_gil_interval_pinned_r03.txt)."""
         return self.env.get_optional_int("SDK_GIL_SWITCH_INTERVAL_MS", 0) / 1000.0
 
+    def gc_gen0_threshold(self) -> int:
+        """Allocations between young-generation collections of the cyclic garbage collector
+        (``SDK_GC_GEN0_THRESHOLD``; default 0 = keep the interpreter's 700). Protobuf-heavy offer
+        cycles allocate tens of thousands of objects; each collection pauses whichever thread is
+        allocating, which is often the offer loop."""
+        return self.env.get_optional_int("SDK_GC_GEN0_THRESHOLD", 0)
+
     def cpu_set(self) -> Optional[list]:
         """CPUs the scheduler process runs on (``SDK_CPU_SET``, a Linux cpu list such as ``4-7`` or
         ``2,3,8-9``; unset = wherever the OS puts it). Applied when the framework starts, so every
