@@ -26,6 +26,7 @@ def gpu_check_runner(device_map=None):
         if device_map is not None:
             dev = device_map(dev)
         return gpu_health.readiness_probe(dev)["healthy"]
+    run.inline = True   # one native call (~0.07 ms, interpreter released): the agent runs it itself
     return run
 
 
@@ -139,6 +140,7 @@ def _run_distributed(args, rank, world, local_rank, use_gpu, dist):
 
     def local_runner(task_info, devices):
         return check({})[0]
+    local_runner.inline = True   # the local probe (or the synthetic pass) is one short call
 
     runners = [local_runner] + [agent_link.RemoteCheckRunner(r) for r in remotes]
     bench = DeployBench(world, profile=args.profile, agent_runners=runners, gpu_devices=list(range(world)),
