@@ -74,9 +74,11 @@ class PersistentLaunchRecorder:
             if status is not None:
                 statuses.append((info.name, status))
         if working:
-            self.state_store.store_tasks(list(working.values()))
-        for name, status in statuses:
-            self.state_store.store_status(name, status)
+            # TaskInfos and their STAGING statuses in one transaction when they fit one batch
+            self.state_store.store_tasks(list(working.values()), statuses)
+        else:
+            for name, status in statuses:
+                self.state_store.store_status(name, status)
 
     def _pod_instance(self, info: P.TaskInfo) -> Optional[PodInstance]:
         try:

@@ -15,7 +15,7 @@ status whose TaskID differs from the stored one (other than the synthetic STAGIN
 from __future__ import annotations
 
 import logging
-from typing import Collection, Dict, List, Optional
+from typing import Collection, Dict, List, Optional, Tuple
 
 from dcos_commons_amd.mesos import protos as P
 from dcos_commons_amd.storage.persister import Persister, PersisterException, Reason
@@ -107,7 +107,13 @@ class StateStore:
                 f"Property value length {len(value)} exceeds limit of {MAX_VALUE_LENGTH_BYTES} bytes.")
 
     # -- tasks ---------------------------------------------------------------------------
-    def store_tasks(self, tasks: Collection[P.TaskInfo]) -> None:
+    def store_tasks(self, tasks: Collection[P.TaskInfo],
+                    statuses: Collection[Tuple[str, P.TaskStatus]] = ()) -> None:
+        """Stores TaskInfos in batches under 1 MB (StateStore.storeTasks). ``statuses`` (task
+        name, status) are checked as ``store_status`` checks them and, when the TaskInfos fit one
+        batch, written in that same transaction (a launch record is one ZooKeeper multi instead of
+        one for the TaskInfos and one per status); otherwise they follow, one write each."""
+        checked = [(name, st) for name, st in statuses if self._check_status(name, st)]
         batches: List[Dict[str, bytes]] = []
         sizes: List[int] = []
         for t in tasks:
@@ -120,16 +126,22 @@ class StateStore:
             sizes[-1] += len(data)
         if len(batches) > 1:
             self.logger.warning("Grouped %d TaskInfo writes in to %d batches", len(tasks), len(batches))
+        elif checked:
+            if not batches:
+                batches.append({})
+            for name, st in checked:
+                batches[0][self._task_status_path(name)] = st.SerializeToString()
+            checked = []
         for b in batches:
             try:
                 self.persister.set_many(b)
             except PersisterException as e:
                 raise StateStoreException(e.reason, f"Failed to store {len(b)} TaskInfos") from e
+        for name, st in checked:
+            self.store_status(name, st)
 
-    def store_status(self, task_name: str, status: P.TaskStatus,
-                     properties: Optional[Dict[str, bytes]] = None) -> None:
-        """Stores ``status`` (StateStore.storeStatus). ``properties`` are written in the same
-        persister transaction (one ZooKeeper multi instead of a round trip each)."""
+    def _check_status(self, task_name: str, status: P.TaskStatus) -> bool:
+        """The checks ``store_status`` applies before writing (raises on a rejected status)."""
         current = self.fetch_status(task_name)
         from dcos_commons_amd.offer.task_utils import is_terminal
 
@@ -142,6 +154,13 @@ class StateStore:
                 and current.task_id.value != status.task_id.value):
             raise StateStoreException(Reason.NOT_FOUND,
                                       f"Dropping TaskStatus with unknown TaskID: {status.task_id.value}")
+        return True
+
+    def store_status(self, task_name: str, status: P.TaskStatus,
+                     properties: Optional[Dict[str, bytes]] = None) -> None:
+        """Stores ``status`` (StateStore.storeStatus). ``properties`` are written in the same
+        persister transaction (one ZooKeeper multi instead of a round trip each)."""
+        self._check_status(task_name, status)
         try:
             if properties:
                 m = {self._task_status_path(task_name): status.SerializeToString()}

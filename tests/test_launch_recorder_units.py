@@ -248,3 +248,40 @@ def test_record_writes_each_task_once_and_skips_unchanged_peers():
     task_writes = [w for w in p.writes if w.endswith("/TaskInfo")]
     assert task_writes == ["Tasks/pod-0-server/TaskInfo"]  # the peer already holds these resources
     assert store.fetch_status("pod-0-server").state == P.TASK_STAGING
+
+
+def test_launch_record_writes_taskinfos_and_staging_statuses_in_one_transaction():
+    """A launch's TaskInfos and their STAGING statuses go to the persister in one set_many (one
+    ZooKeeper multi); a status the store would reject stops the whole record before any write."""
+    from dcos_commons_amd.state.state_store import StateStore, StateStoreException
+    from dcos_commons_amd.storage.mem_persister import MemPersister
+
+    class Counting(MemPersister):
+        def __init__(self):
+            super().__init__()
+            self.writes = []
+
+        def set_many(self, m):
+            self.writes.append(sorted(m))
+            return super().set_many(m)
+
+        def set(self, path, data):
+            self.writes.append([path])
+            return super().set(path, data)
+
+    p = Counting()
+    ss = StateStore(p)
+    info = P.TaskInfo(name="pod-0-task")
+    info.task_id.value = "svc__pod-0-task__1"
+    st = P.TaskStatus(state=P.TASK_STAGING)
+    st.task_id.CopyFrom(info.task_id)
+    ss.store_tasks([info], [("pod-0-task", st)])
+    assert len(p.writes) == 1 and any(w.endswith("TaskStatus") for w in p.writes[0])
+    assert ss.fetch_status("pod-0-task").state == P.TASK_STAGING
+    # a RUNNING status for another task ID is rejected before anything is written
+    p.writes.clear()
+    bad = P.TaskStatus(state=P.TASK_RUNNING)
+    bad.task_id.value = "svc__pod-0-task__other"
+    with pytest.raises(StateStoreException):
+        ss.store_tasks([info], [("pod-0-task", bad)])
+    assert p.writes == []
