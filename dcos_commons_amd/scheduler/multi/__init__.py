@@ -422,6 +422,19 @@ class MultiServiceEventClient(MesosEventClient):
     def awaiting_reconciliation(self) -> bool:
         return any(s.awaiting_reconciliation() for s in self.manager.all_services())
 
+    def offer_cycle_useful(self) -> bool:
+        """After a readiness result: useful if any service could use a cycle (a service whose last
+        launched step completed also frees the offer discipline for the others); no services:
+        always (deregistration)."""
+        services = self.manager.all_services()
+        if not services:
+            return True
+        for s in services:
+            useful = getattr(s, "offer_cycle_useful", None)
+            if useful is None or useful():
+                return True
+        return False
+
     def task_status(self, status) -> TaskStatusResponse:
         s = self.manager.get_matching_service(status)
         if s is None:

@@ -841,3 +841,31 @@ def test_offer_cycle_useful_follows_the_plans():
     assert useful(PM(Status.STARTED), PM(Status.WAITING))                     # e.g. held back by a conflict
     assert useful(PM(Status.COMPLETE, Status.COMPLETE), PM())                 # all done: time to suppress
     assert useful(PM(Status.STARTED, Status.DELAYED))
+
+
+def test_multi_service_offer_cycle_useful_is_any_service():
+    from dcos_commons_amd.scheduler.multi import MultiServiceEventClient
+
+    class S:
+        def __init__(self, useful):
+            self.useful = useful
+
+        def offer_cycle_useful(self):
+            return self.useful
+
+    class M:
+        def __init__(self, services):
+            self.services = services
+
+        def all_services(self):
+            return self.services
+
+    c = MultiServiceEventClient.__new__(MultiServiceEventClient)
+    c.manager = M([])
+    assert c.offer_cycle_useful()                     # nothing left: deregistration may proceed
+    c.manager = M([S(False), S(False)])
+    assert not c.offer_cycle_useful()
+    c.manager = M([S(False), S(True)])                # e.g. a service waiting on the offer discipline
+    assert c.offer_cycle_useful()
+    c.manager = M([S(False), object()])               # a service without the predicate: always
+    assert c.offer_cycle_useful()
