@@ -45,7 +45,9 @@ def ask(socket_path: str, device: int, inject: int = 0, timeout_s: float = 30.0)
 class ProbeService:
     """``amd-gpu-probed`` as a child process, listening on ``socket_path``. ``warm`` probes every
     visible device at start (runtime, code objects and contexts ready before the first pod);
-    the daemon exits with this process (``--parent-death``) or on ``stop()``."""
+    the daemon exits with this process (``--parent-death``) or on ``stop()``. The parent-death
+    signal follows the *thread* that started it (Linux ``PR_SET_PDEATHSIG``): start the service
+    from a thread that lives as long as the service should, e.g. the main thread."""
 
     def __init__(self, socket_path: str, binary: str = SERVICE_BINARY, warm: bool = True,
                  env: Optional[Dict[str, str]] = None, log_path: Optional[str] = None):
