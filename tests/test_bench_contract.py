@@ -38,6 +38,7 @@ def _check(rec, n, steps, warmup):
     assert rec["config"]["pods"] == n and rec["config"]["agents"] == n
     assert rec["value"] > 0 and rec["ms_per_step"] > 0
     assert rec["mttr_restart_s"]["mean"] > 0 and rec["mttr_replace_s"]["mean"] > 0
+    assert 0 < rec["deploy_from_subscribed_s"]["mean"] < rec["value"]
 
 
 def test_bench_single_process():

@@ -157,3 +157,5 @@ def test_bench_cycle_cpu(profile):
 
     res = DeployBench(2, profile=profile, allocation_interval_s=0.05, timeout_s=60).run_cycle()
     assert res.deploy_s < 10 and res.mttr_restart_s < 15 and res.mttr_replace_s < 15
+    # BASELINE.md's window starts at SUBSCRIBED, inside the headline's (which starts at construction)
+    assert 0 < res.deploy_from_subscribed_s < res.deploy_s
