@@ -2,17 +2,25 @@
 
 Reference: sdk/.../specification/yaml/Raw*.java (21 files) and RawServiceSpec.java:31-112:
 Jackson YAML with ``STRICT_DUPLICATE_DETECTION`` (duplicate keys are errors at every level,
-``WriteOnceLinkedHashMap.java:18``) and unknown properties rejected. Mapping order is preserved
+``WriteOnceLinkedHashMap.java:18``). Unknown properties are rejected at every level except the pod:
+``RawPod.java:18`` is the one Raw* class annotated ``@JsonIgnoreProperties(ignoreUnknown = true)``,
+so pod-level keys such as helloworld ``gpu_resource.yml``'s ``container:`` block or
+``graceful-shutdown.yml``'s ``user:`` are ignored (with a WARN naming them here). The other 20 Raw*
+classes keep Jackson's default ``FAIL_ON_UNKNOWN_PROPERTIES``. Mapping order is preserved
 (pods/tasks/phases keep YAML order, which drives plan order).
 """
 from __future__ import annotations
 
+import logging
 import os
 from typing import Any, Dict, List, Mapping, Optional
 
 import yaml
 
 from .template_utils import MissingValue, render_mustache, validate_missing_values
+
+
+LOGGER = logging.getLogger(__name__)
 
 
 class RawSpecError(ValueError):
@@ -75,6 +83,10 @@ TLS_KEYS = {"name", "type"}
 RANGE_KEYS = {"begin", "end"}
 
 
+# Raw* levels that ignore unknown keys instead of failing: only RawPod (RawPod.java:18).
+LENIENT_LEVELS = frozenset({"pod"})
+
+
 def _check(node: Any, allowed, where: str) -> Dict[str, Any]:
     if node is None:
         return {}
@@ -84,6 +96,19 @@ def _check(node: Any, allowed, where: str) -> Dict[str, Any]:
     if unknown:
         raise RawSpecError(f"Unrecognized field(s) {sorted(unknown)} in {where} (known: {sorted(allowed)})")
     return node
+
+
+def _check_lenient(node: Any, allowed, where: str) -> Dict[str, Any]:
+    """``@JsonIgnoreProperties(ignoreUnknown = true)``: unknown keys are dropped, not errors."""
+    if node is None:
+        return {}
+    if not isinstance(node, dict):
+        raise RawSpecError(f"Expected a mapping for {where}, got {type(node).__name__}")
+    unknown = [k for k in node if k not in allowed]
+    if not unknown:
+        return node
+    LOGGER.warning("Ignoring unrecognized field(s) %s in %s", unknown, where)
+    return {k: v for k, v in node.items() if k in allowed}
 
 
 def _map_of(node: Any, allowed, where: str) -> Dict[str, Dict[str, Any]]:
@@ -114,7 +139,7 @@ class RawServiceSpec:
         self.scheduler: Dict[str, Any] = _check(data.get("scheduler"), SCHEDULER_KEYS, "scheduler")
         self.pods: Dict[str, Dict[str, Any]] = {}
         for pod_name, pod in (data.get("pods") or {}).items():
-            pod = _check(pod, POD_KEYS, f"pods.{pod_name}")
+            pod = _check_lenient(pod, POD_KEYS, f"pods.{pod_name}")
             tasks = {}
             for tname, task in (pod.get("tasks") or {}).items():
                 task = _check(task, TASK_KEYS, f"pods.{pod_name}.tasks.{tname}")

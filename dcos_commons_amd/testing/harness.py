@@ -283,8 +283,16 @@ class SendOffer(Send):
         return self
 
     @staticmethod
-    def _unreserved(name: str, value: P.Value, mount_root: Optional[str] = None) -> P.Resource:
-        r = P.Resource(name=name, type=value.type, role="*")
+    def _unreserved(name: str, value: P.Value, mount_root: Optional[str] = None,
+                    pre_reserved_role: Optional[str] = None, profile: Optional[str] = None) -> P.Resource:
+        """An unreserved resource, or with ``pre_reserved_role`` one statically reserved to that role
+        (refinement form: a STATIC entry at the bottom of ``reservations``, as an agent started with
+        ``--resources=...(role)`` offers it). ``profile`` marks a MOUNT disk as coming from that CSI
+        volume profile, so ``profiles: [...]`` volumes can match it."""
+        role = pre_reserved_role if pre_reserved_role not in (None, "", "*") else None
+        r = P.Resource(name=name, type=value.type) if role else P.Resource(name=name, type=value.type, role="*")
+        if role:
+            r.reservations.add(type=P.Resource.ReservationInfo.STATIC, role=role)
         if value.type == P.Value.SCALAR:
             r.scalar.CopyFrom(value.scalar)
         elif value.type == P.Value.RANGES:
@@ -292,6 +300,8 @@ class SendOffer(Send):
         if mount_root is not None:
             r.disk.source.type = P.Resource.DiskInfo.Source.MOUNT
             r.disk.source.mount.root = mount_root
+            if profile:
+                r.disk.source.profile = profile
         return r
 
     def _offer(self, sim: "_Sim") -> P.Offer:
@@ -329,9 +339,12 @@ class SendOffer(Send):
         if not self.pod_to_reuse or self.with_unreserved:
             from dcos_commons_amd.specification.specs import VolumeType
 
+            pre_role = getattr(pod, "pre_reserved_role", None)
+
             def vol(v):
                 mount = "/mnt/" + v.container_path if v.type == VolumeType.MOUNT else None
-                return self._unreserved("disk", v.value, mount)
+                profile = v.profiles[0] if mount is not None and v.profiles else None
+                return self._unreserved("disk", v.value, mount, pre_role, profile)
             for v in pod.volumes:
                 o.resources.add().CopyFrom(vol(v))
             from dcos_commons_amd.specification.specs import PortSpec
@@ -343,15 +356,16 @@ class SendOffer(Send):
                         # agents offer port *ranges*: dynamic ports are claimed from them
                         dynamic_ports = True
                         for rg in r.ranges:
-                            o.resources.add().CopyFrom(self._unreserved("ports", _ranges(rg.begin, rg.end)))
+                            o.resources.add().CopyFrom(self._unreserved("ports", _ranges(rg.begin, rg.end),
+                                                                        pre_reserved_role=pre_role))
                         continue
-                    o.resources.add().CopyFrom(self._unreserved(r.name, r.value))
+                    o.resources.add().CopyFrom(self._unreserved(r.name, r.value, pre_reserved_role=pre_role))
                 for v in t.resource_set.volumes:
                     o.resources.add().CopyFrom(vol(v))
             if dynamic_ports:
-                o.resources.add().CopyFrom(self._unreserved("ports", _ranges(10000, 10999)))
+                o.resources.add().CopyFrom(self._unreserved("ports", _ranges(10000, 10999), pre_reserved_role=pre_role))
             for name, value in sim.cfg.executor_resources().items():
-                o.resources.add().CopyFrom(self._unreserved(name, value))
+                o.resources.add().CopyFrom(self._unreserved(name, value, pre_reserved_role=pre_role))
         o.resources.extend(self.extra)
         o.agent_id.value = agent or ("test-agent-" + str(uuid.uuid4()))
         for k, v in sorted(self.attributes.items()):
@@ -710,11 +724,19 @@ class ServiceTestRunner:
         self.prior_accepts: List = []
 
     @staticmethod
-    def for_framework(name: str, spec_file: str = "svc.yml") -> "ServiceTestRunner":
-        """Spec + Universe package of ``frameworks/<name>`` (the reference's default runner layout)."""
-        root = os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))),
-                            "frameworks", name)
-        return ServiceTestRunner(os.path.join(root, "specs", spec_file), universe_dir=os.path.join(root, "universe"))
+    def for_framework(name: str, spec_file: str = "svc.yml", root: Optional[str] = None) -> "ServiceTestRunner":
+        """Spec + Universe package of ``frameworks/<name>`` (the reference's default runner layout).
+
+        ``root`` points at another framework tree instead, e.g. the reference's unchanged
+        ``frameworks/<name>``: there the spec lives in ``src/main/dist`` (ServiceTestRunner.java
+        ``getDistDir``), here in ``specs``."""
+        if root is None:
+            root = os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))),
+                                "frameworks", name)
+        spec_dir = os.path.join(root, "specs")
+        if not os.path.isdir(spec_dir):
+            spec_dir = os.path.join(root, "src", "main", "dist")
+        return ServiceTestRunner(os.path.join(spec_dir, spec_file), universe_dir=os.path.join(root, "universe"))
 
     def set_options(self, *key_vals, **options) -> "ServiceTestRunner":
         """Universe package options, e.g. ``set_options("service.user", "foo")``."""
@@ -788,6 +810,10 @@ class ServiceTestRunner:
         cfg_env = dict(sched_env) if self.universe_dir is not None else {}
         cfg_env.update({"PORT_API": "0", "SDK_EVENT_DRIVEN": "false", "SDK_OFFER_HOLD_S": "0"})
         cfg_env.update(self.scheduler_env)
+        if "DCOS_SERVICE_ACCOUNT_CREDENTIAL" not in cfg_env:
+            # the reference runner's mocked SchedulerConfig hands out a (null) token provider
+            # without failing (ServiceTestRunner.java:296), so TLS specs pass TLSRequiresServiceAccount
+            cfg_env.setdefault("SDK_DCOS_AUTH_TOKEN", "service-test-runner-token")
         cfg = SchedulerConfig.for_testing(**cfg_env)
         raw = self.raw
         spec = self.spec

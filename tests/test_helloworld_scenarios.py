@@ -20,10 +20,11 @@ ENV = dict(FRAMEWORK_NAME="hello-world", FRAMEWORK_PRINCIPAL="hello-world-princi
            HELLO_VERSION="1", HELLO_SECRET1="hello-world/secret1", HELLO_SECRET2="hello-world/secret2", WORLD_SECRET1="hello-world/secret1",
            WORLD_SECRET2="hello-world/secret2", WORLD_SECRET3="hello-world/secret3",
            DISCOVERY_TASK_PREFIX="custom", GPU_PROBE_CMD="true", PRE_RESERVED_ROLE="slave_public",
-           TASKCFG_ALL_GREETING="hi", TASKCFG_HELLO_TARGET="everyone")
+           TASKCFG_ALL_GREETING="hi", TASKCFG_HELLO_TARGET="everyone", HELLO_VOLUME_PROFILE="xfs")
 
-# scenarios that need resources the generic unreserved offers do not carry
-RENDER_ONLY = {"pre-reserved.yml", "pre-reserved-sidecar.yml", "profile-mount-volume.yml", "tls.yml"}
+# scenarios that need a DC/OS CA (tests/test_tls.py and test_reference_conformance.py deploy it);
+# pre-reserved and profiled-disk scenarios get offers carrying those resources (harness SendOffer)
+RENDER_ONLY = {"tls.yml"}
 ALL = sorted(f for f in os.listdir(SPECS) if f.endswith(".yml"))
 
 
