@@ -61,20 +61,54 @@ def _behavior() -> TaskBehavior:
     return TaskBehavior(TaskTiming(honor_check_delays=False), overrides={k: finish for k in _FINISHING})
 
 
-def _scheduler_env(framework: str, **extra: str) -> Dict[str, str]:
+# Where the reference's unchanged framework packages are looked for: $SDK_REFERENCE_ROOT, the
+# reference checkout, or a staged copy of its frameworks/ (scripts/stage_reference_inputs.sh; the GPU
+# box gets only the repository tree, so the copy travels in a gitignored directory of it).
+REFERENCE_ROOTS = (os.environ.get("SDK_REFERENCE_ROOT", ""), "/root/reference", os.path.join(ROOT, "ref_inputs"))
+
+
+def reference_framework_root(framework: str) -> Optional[str]:
+    for root in REFERENCE_ROOTS:
+        d = os.path.join(root, "frameworks", framework) if root else ""
+        if d and os.path.isfile(os.path.join(d, "src", "main", "dist", "svc.yml")):
+            return d
+    return None
+
+
+def framework_root(framework: str, spec_set: str) -> str:
+    """``spec_set="reference"``: the reference's unchanged ``svc.yml`` (+ config templates) and
+    ``universe/`` package; ``"repo"``: this repository's rewritten, lighter package."""
+    if spec_set == "reference":
+        root = reference_framework_root(framework)
+        if root is None:
+            raise FileNotFoundError(f"no reference frameworks/{framework} found in {REFERENCE_ROOTS}")
+        return root
+    if spec_set != "repo":
+        raise ValueError(f"unknown spec set {spec_set!r}")
+    return os.path.join(ROOT, "frameworks", framework)
+
+
+def spec_path(root: str) -> str:
+    repo_layout = os.path.join(root, "specs", "svc.yml")
+    return repo_layout if os.path.isfile(repo_layout) else os.path.join(root, "src", "main", "dist", "svc.yml")
+
+
+def _scheduler_env(root: str, **extra: str) -> Dict[str, str]:
     from dcos_commons_amd.testing.cosmos import render_scheduler_environment
 
-    env = render_scheduler_environment(os.path.join(ROOT, "frameworks", framework, "universe"), {}, {})
+    env = render_scheduler_environment(os.path.join(root, "universe"), {}, {})
     env.update(extra)
     return env
 
 
 class FrameworkBench:
     def __init__(self, framework: str, profile: str = "mi355x", allocation_interval_s: float = 1.0,
-                 timeout_s: float = 120.0):
+                 timeout_s: float = 120.0, spec_set: str = "reference"):
         if framework not in ("cassandra", "hdfs"):
             raise ValueError(f"unknown framework {framework!r}")
         self.framework = framework
+        self.spec_set = spec_set
+        self.root = framework_root(framework, spec_set)
         self.profile = profile
         self.allocation_interval_s = allocation_interval_s
         self.timeout_s = timeout_s
@@ -122,7 +156,7 @@ class FrameworkBench:
         return master
 
     def _builder(self, env: Dict[str, str], cfg: SchedulerConfig, persister):
-        spec = os.path.join(ROOT, "frameworks", self.framework, "specs", "svc.yml")
+        spec = spec_path(self.root)
         if self.framework == "cassandra":
             from dcos_commons_amd.models import cassandra as m
         else:
@@ -152,7 +186,7 @@ class FrameworkBench:
 
     def _cassandra(self) -> FrameworkCycle:
         t_cycle = time.perf_counter()
-        env = _scheduler_env("cassandra", NODE_COUNT="3")
+        env = _scheduler_env(self.root, NODE_COUNT="3")
         cfg, persister, master = self._config(), MemPersister(), self._master(3)
         runner = None
         try:
@@ -191,7 +225,7 @@ class FrameworkBench:
 
     def _hdfs(self) -> FrameworkCycle:
         t_cycle = time.perf_counter()
-        env = _scheduler_env("hdfs")
+        env = _scheduler_env(self.root)
         cfg, persister, master = self._config(), MemPersister(), self._master(8)
         runner = None
         try:
@@ -244,15 +278,27 @@ def main(argv: Optional[List[str]] = None) -> int:
     ap.add_argument("--profile", choices=sorted(PROFILES), default="mi355x")
     ap.add_argument("--cycles", type=int, default=3)
     ap.add_argument("--allocation-interval", type=float, default=1.0)
+    ap.add_argument("--specs", choices=["reference", "repo", "both"], default="both",
+                    help="reference: the reference's unchanged svc.yml + universe/ (the BASELINE configs); "
+                         "repo: this repository's rewritten packages")
     args = ap.parse_args(argv)
-    for fw in (["cassandra", "hdfs"] if args.framework == "all" else [args.framework]):
-        bench = FrameworkBench(fw, args.profile, args.allocation_interval)
+    spec_sets = ["reference", "repo"] if args.specs == "both" else [args.specs]
+    runs = [(fw, ss) for fw in (["cassandra", "hdfs"] if args.framework == "all" else [args.framework])
+            for ss in spec_sets]
+    for fw, ss in runs:
+        if ss == "reference" and reference_framework_root(fw) is None:
+            print(json.dumps({"framework": fw, "specs": ss, "skipped": "reference package not found"}), flush=True)
+            continue
+        bench = FrameworkBench(fw, args.profile, args.allocation_interval, spec_set=ss)
         cycles = [bench.run_cycle() for _ in range(args.cycles)]
         second = cycles[0].second_name
-        out = {"framework": fw, "profile": args.profile, "cycles": args.cycles, "tasks": cycles[0].tasks,
+        out = {"framework": fw, "specs": ss, "spec_path": spec_path(bench.root), "profile": args.profile,
+               "cycles": args.cycles, "tasks": cycles[0].tasks,
                "deploy_s": {"mean": round(sum(c.deploy_s for c in cycles) / len(cycles), 6),
+                            "min": round(min(c.deploy_s for c in cycles), 6),
                             "max": round(max(c.deploy_s for c in cycles), 6)},
                second: {"mean": round(sum(c.second_s for c in cycles) / len(cycles), 6),
+                        "min": round(min(c.second_s for c in cycles), 6),
                         "max": round(max(c.second_s for c in cycles), 6)},
                "data": "synthetic task payloads (LocalMaster), readiness delays not honoured"}
         print(json.dumps(out), flush=True)

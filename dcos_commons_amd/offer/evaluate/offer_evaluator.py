@@ -12,6 +12,7 @@ pass a pre-fetched task map (``all_tasks``) so a whole offer cycle touches stora
 """
 from __future__ import annotations
 
+from collections import OrderedDict
 from typing import Dict, List, Optional, Sequence
 
 from dcos_commons_amd import trace
@@ -110,7 +111,32 @@ class OfferEvaluator:
         self.tls_stage_factory = tls_stage_factory
         self._framework_id: Optional[str] = None
         self._executor_specs: Dict[tuple, List[ResourceSpec]] = {}
+        # untouched PodInfoBuilder templates, reused across offer cycles (see _template)
+        self._templates: "OrderedDict[tuple, tuple]" = OrderedDict()
         self.logger = get_logger(__name__, resource_namespace)
+
+    _TEMPLATE_CACHE_SIZE = 512
+
+    def _template(self, requirement: PodInstanceRequirement, target_config, override_map,
+                  fid_proto: P.FrameworkID) -> PodInfoBuilder:
+        """The offer-independent PodInfoBuilder of a requirement: every task's command,
+        environment, checks, labels and container info, and the executor. Building it renders the
+        pod's whole task environment (a reference hdfs or cassandra task carries hundreds of
+        variables), so it is built once per (pod instance, target config, requirement env, goal
+        overrides) and every evaluation -- each offer cycle, each offer -- works on a copy."""
+        pi = requirement.pod_instance
+        key = (pi.pod.type, pi.index, str(target_config), tuple(sorted(requirement.environment.items())),
+               tuple(sorted((k, str(v)) for k, v in override_map.items())), fid_proto.value)
+        hit = self._templates.get(key)
+        if hit is not None and hit[0] is pi.pod:
+            self._templates.move_to_end(key)
+            return hit[1]
+        tpl = PodInfoBuilder(requirement, self.service_name, target_config, self.template_url_factory,
+                             self.scheduler_config, (), fid_proto, override_map)
+        self._templates[key] = (pi.pod, tpl)
+        if len(self._templates) > self._TEMPLATE_CACHE_SIZE:
+            self._templates.popitem(last=False)
+        return tpl
 
     def _executor_specs_for(self, role: str, principal: str, pre_reserved_role: str) -> List[ResourceSpec]:
         """The executor's resource specs (immutable) for one role/principal, built once."""
@@ -157,7 +183,8 @@ class OfferEvaluator:
                         for ts in pi.pod.tasks}
         target_config = self.get_target_config(requirement, this_pod)
         required = _required_reservations(stages)
-        prototype = None
+        template = None
+        prior_ports = None
         for i, offer in enumerate(offers):
             if required:
                 missing = required.difference(get_resource_id(r) for r in offer.resources)
@@ -173,11 +200,13 @@ class OfferEvaluator:
                     self._track(requirement, False, offer, lambda o=o: "\n".join(_outcome_lines(o)), [o])
                     continue
             pool = MesosResourcePool(offer, role)
-            # one offer-independent build per requirement; each offer's stages work on a copy
-            if prototype is None:
-                prototype = PodInfoBuilder(requirement, self.service_name, target_config, self.template_url_factory,
-                                           self.scheduler_config, this_pod.values(), fid_proto, override_map)
-            builder = prototype.clone() if i + 1 < len(offers) else prototype
+            # each offer's stages work on a copy of the cached offer-independent template, with
+            # this pod's prior ports
+            if template is None:
+                template = self._template(requirement, target_config, override_map, fid_proto)
+                prior_ports = PodInfoBuilder.prior_ports(this_pod.values())
+            builder = template.clone()
+            builder.ports_by_task = prior_ports
             outcomes = []
             failed = 0
             for stage in stages:

@@ -77,19 +77,28 @@ class PodInfoBuilder:
                 if rs.name == constants.PORTS_RESOURCE_TYPE and rs.value.ranges.range[0].begin > 0:
                     self.assigned_overlay_ports.add(int(rs.value.ranges.range[0].begin))
         self.executor_builder = self._executor_info(pi, framework_id, scheduler_config)
-        self.ports_by_task: Dict[str, Dict[str, int]] = {}
-        for t in current_pod_tasks:
-            if not L.TaskLabelReader(t).is_permanently_failed():
-                self.ports_by_task[t.name] = {p.name: int(p.number) for p in t.discovery.ports.ports if p.name}
+        self.ports_by_task: Dict[str, Dict[str, int]] = self.prior_ports(current_pod_tasks)
         for tb in self.task_builders.values():
             self._validate(tb)
 
+    @staticmethod
+    def prior_ports(current_pod_tasks) -> Dict[str, Dict[str, int]]:
+        """Ports the pod's current (not permanently failed) tasks hold, by task and port name: a
+        relaunch keeps them. Read-only once built; builders of one evaluation share it."""
+        out: Dict[str, Dict[str, int]] = {}
+        for t in current_pod_tasks:
+            if not L.TaskLabelReader(t).is_permanently_failed():
+                out[t.name] = {p.name: int(p.number) for p in t.discovery.ports.ports if p.name}
+        return out
+
     def clone(self) -> "PodInfoBuilder":
         """A builder in the state this one was constructed in, for the next offer. Nothing in the
-        construction depends on the offer, so the evaluator builds the task/executor templates once
-        per requirement and each offer's stages mutate a copy (protobuf ``CopyFrom``) instead of
-        rebuilding every task's command, environment, checks and container info (a cassandra node
-        pod: 13 tasks). Call it on a builder no stage has touched."""
+        construction but ``ports_by_task`` depends on the offer or the pod's current tasks, so the
+        evaluator keeps one untouched template per (pod instance, target config, requirement
+        environment, goal overrides) across offer cycles, and each offer's stages mutate a copy
+        (protobuf ``CopyFrom``) instead of rebuilding every task's command, environment, checks and
+        container info (a reference hdfs/cassandra task carries hundreds of environment variables).
+        Call it on a builder no stage has touched."""
         c = PodInfoBuilder.__new__(PodInfoBuilder)
         c.pod_instance = self.pod_instance
         c.assigned_overlay_ports = set(self.assigned_overlay_ports)
@@ -166,18 +175,24 @@ class PodInfoBuilder:
         w.set_additional_labels(ts.labels)
         w.apply()
         # the command, health check and readiness check all start from the same task environment
-        base_env = L.env_from_map(get_task_environment(service_name, pi, ts, scheduler_config))
+        env_map = get_task_environment(service_name, pi, ts, scheduler_config)
+        base_env = L.env_from_map(env_map)
         if ts.command is not None:
             cmd = t.command
-            cmd.environment.CopyFrom(base_env)
+            if ts.config_files:
+                # EnvUtils.withEnvVar per config file (PodInfoBuilder.java:279-283): keyed by name,
+                # sorted; applied to the map in one pass rather than re-sorting the proto per file
+                cmd_map = dict(env_map)
+                for config in ts.config_files:
+                    cmd_map[CONFIG_TEMPLATE_KEY_FORMAT % L.to_env_name(config.name)] = \
+                        f"{config_template_download_path(config)},{config.relative_path}"
+                cmd.environment.CopyFrom(L.env_from_map(cmd_map))
+            else:
+                cmd.environment.CopyFrom(base_env)
             if override == GoalStateOverride.PAUSED:
                 cmd.value = scheduler_config.pause_override_cmd()
             else:
                 cmd.value = ts.command.value
-            for config in ts.config_files:
-                cmd.environment.CopyFrom(L.with_env_var(
-                    cmd.environment, CONFIG_TEMPLATE_KEY_FORMAT % L.to_env_name(config.name),
-                    f"{config_template_download_path(config)},{config.relative_path}"))
             for k, v in environment.items():
                 cmd.environment.variables.add(name=k, value=v)
             if override == GoalStateOverride.PAUSED:

@@ -456,10 +456,12 @@ class LaunchEvaluationStage(OfferEvaluationStage):
             w.set_region(offer.domain.fault_domain.region.name).set_zone(offer.domain.fault_domain.zone.name)
         w.apply()
         _update_fault_domain_env(t, offer)
-        snapshot = P.TaskInfo()
-        snapshot.CopyFrom(t)
-        exec_snapshot = P.ExecutorInfo()
-        exec_snapshot.CopyFrom(e)
+        # no snapshot copies: the builder belongs to this one offer's evaluation, and no stage
+        # after a task's launch stage touches that task or the executor (executor, pod-volume and
+        # TLS stages run first; each later resource-set stage writes only its own tasks). The
+        # LAUNCH_GROUP operation copies both, and the store recommendation copies them when the
+        # launch is recorded.
+        snapshot, exec_snapshot = t, e
         if self.should_launch:
             return EvaluationOutcome.pass_(
                 self, "Added launch operation for %s", self.task_spec_name,

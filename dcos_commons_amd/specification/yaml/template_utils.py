@@ -57,6 +57,7 @@ def _tokenize(template: str) -> List[Tuple[int, str, int]]:
     pos = 0
     raw_tokens: List[list] = []  # [kind, value, start, end, line]
     n = len(template)
+    line, counted_to = 1, 0  # line of ``counted_to``, advanced incrementally (not rescanned per tag)
     while pos < n:
         start = template.find(otag, pos)
         if start < 0:
@@ -64,7 +65,8 @@ def _tokenize(template: str) -> List[Tuple[int, str, int]]:
             break
         if start > pos:
             raw_tokens.append([_TEXT, template[pos:start], pos, start, 0])
-        line = template.count("\n", 0, start) + 1
+        line += template.count("\n", counted_to, start)
+        counted_to = start
         inner_start = start + len(otag)
         if otag == "{{" and template.startswith("{", inner_start):
             end = template.find("}" + ctag, inner_start)
@@ -112,9 +114,18 @@ def _tokenize(template: str) -> List[Tuple[int, str, int]]:
             before = template[ls:t[2]]
             after = template[t[3]:le_eff]
             if before.strip() == "" and after.strip() == "":
-                # make sure no other tag shares the line
-                others = [o for o in raw_tokens if o is not t and o[0] != _TEXT and ls <= o[2] < le_eff + 1]
-                if not others:
+                # make sure no other tag shares the line (tokens are in position order, so only
+                # the neighbours up to the line's bounds need looking at)
+                alone = True
+                j = i - 1
+                while alone and j >= 0 and raw_tokens[j][2] >= ls:
+                    alone = raw_tokens[j][0] == _TEXT
+                    j -= 1
+                j = i + 1
+                while alone and j < len(raw_tokens) and raw_tokens[j][2] < le_eff + 1:
+                    alone = raw_tokens[j][0] == _TEXT
+                    j += 1
+                if alone:
                     t.append((ls, le_eff + 1 if le >= 0 else le_eff))
     # rebuild text tokens honoring removed ranges
     removed = [t[5] for t in raw_tokens if len(t) > 5]
@@ -246,10 +257,25 @@ def _coerce_env(values: Mapping[str, Any]) -> Dict[str, Any]:
     return out
 
 
+# parsed templates by content: a scheduler renders the same svc.yml and config templates on every
+# start, config update and (for tasks' config files) validation pass
+_PARSED: Dict[str, list] = {}
+_PARSED_MAX = 256
+
+
+def _parsed(content: str) -> list:
+    nodes = _PARSED.get(content)
+    if nodes is None:
+        nodes, _ = _parse(_tokenize(content))
+        if len(_PARSED) >= _PARSED_MAX:
+            _PARSED.clear()
+        _PARSED[content] = nodes
+    return nodes
+
+
 def render_mustache(template_name: str, content: str, values: Mapping[str, Any],
                     missing_values: Optional[List[MissingValue]] = None) -> str:
-    tokens = _tokenize(content)
-    nodes, _ = _parse(tokens)
+    nodes = _parsed(content)
     out: List[str] = []
     missing: List[MissingValue] = [] if missing_values is None else missing_values
     _render(nodes, [_coerce_env(values)], out, missing)

@@ -576,3 +576,28 @@ def test_in_place_relaunch_skips_offers_without_its_reservations():
     full = offer(*(_executor_reserved(first) + [_reserved(first, "cpus"), _reserved(first, "mem")]), oid="full")
     again = f.evaluate([other_agent, full])
     assert ops(again) == [L, None] and again[0].offer.id.value == "full"
+
+
+def test_pod_templates_are_reused_across_evaluations_without_leaking_offer_state():
+    """The evaluator keeps one untouched PodInfoBuilder template per (pod instance, target config,
+    requirement env, goal overrides) and each evaluation works on a copy: task IDs, agent IDs,
+    port env vars and reservations of one evaluation never reach the next."""
+    f = Fixture(server(extra="ports:\n  http:\n    port: 0\n    env-key: PORT_HTTP\n"))
+    o1 = complete_offer(scalar("cpus", 1.0), ranges("ports", (5000, 5000)), agent="a1", oid="o1")
+    o2 = complete_offer(scalar("cpus", 1.0), ranges("ports", (6000, 6000)), agent="a2", oid="o2")
+    first = of(f.evaluate([o1]), LaunchOfferRecommendation)[0].task_info
+    assert len(f.evaluator._templates) == 1
+    tpl = next(iter(f.evaluator._templates.values()))[1]
+    second = of(f.evaluate([o2]), LaunchOfferRecommendation)[0].task_info
+    assert len(f.evaluator._templates) == 1 and next(iter(f.evaluator._templates.values()))[1] is tpl
+    assert first.task_id.value != second.task_id.value
+    assert (first.agent_id.value, second.agent_id.value) == ("a1", "a2")
+    assert env_to_map(first.command.environment)["PORT_HTTP"] == "5000"
+    assert env_to_map(second.command.environment)["PORT_HTTP"] == "6000"
+    untouched = tpl.get_task_builder("server")
+    assert not untouched.task_id.value and not untouched.resources and "PORT_HTTP" not in env_to_map(
+        untouched.command.environment)
+    # another pod index, requirement environment or target config is another template
+    f.evaluator.evaluate(PodInstanceRequirement(PodInstance(f.spec.pods[0], 0), ["server"],
+                                                environment={"EXTRA": "1"}), [o1])
+    assert len(f.evaluator._templates) == 2
