@@ -42,8 +42,14 @@ def parse_args(argv=None):
                     help="scheduler flag override on top of --profile (A/B experiments)")
     ap.add_argument("--no-pin", action="store_true",
                     help="do not pin each rank to its own slice of the allowed CPUs")
+    ap.add_argument("--reference-steps", type=int, default=None,
+                    help="cycles of the reference's unchanged gpu_resource.yml (default serial deploy) run after "
+                         "the timed region and reported as `reference_spec` (default: --steps; 0 = skip)")
     ap.add_argument("--verbose", action="store_true")
-    return ap.parse_args(argv)
+    args = ap.parse_args(argv)
+    if args.reference_steps is None:
+        args.reference_steps = args.steps
+    return args
 
 
 def pin_cpus(local_rank: int, local_world: int, per: int = 4, skip: int = 4) -> list:

@@ -68,18 +68,56 @@ def helloworld_env(n_pods: int, gpus_per_pod: int, probe_cmd: str) -> Dict[str, 
     }
 
 
+def reference_spec(name: str) -> Optional[str]:
+    """Path of the reference's unchanged helloworld example ``name`` (e.g. ``gpu_resource.yml``),
+    from $SDK_REFERENCE_ROOT, the reference checkout or the staged ``ref_inputs/`` copy."""
+    for root in (os.environ.get("SDK_REFERENCE_ROOT", ""), "/root/reference", os.path.join(ROOT, "ref_inputs")):
+        p = os.path.join(root, "frameworks", "helloworld", "src", "main", "dist", name) if root else ""
+        if p and os.path.isfile(p):
+            return p
+    return None
+
+
+def agent_specs_from_inventory(devices: List[int], inventory=None, hostname="mi355x-agent-{i}") -> List[AgentSpec]:
+    """One agent per entry of ``devices`` (a device index of this node), its resources and
+    attributes (``gpu_model``, ``gpu_arch``, ``xgmi_hive``) from node discovery (``ops.gpu``):
+    the devices this node really has, or a synthetic MI355X inventory where there is no driver."""
+    from dcos_commons_amd.ops import gpu as G
+
+    inv = inventory if inventory is not None else G.node_inventory(max(devices) + 1 if devices else 0)
+    return [AgentSpec.from_gpu_inventory(hostname.format(i=i), inv, devices=[dev], cpus=16, mem=65536, disk=100000)
+            for i, dev in enumerate(devices)]
+
+
+def agent_spec_from_registration(info: Dict, index: int) -> AgentSpec:
+    """The agent a remote rank registered over ``parallel.agent_link``: its hostname, the device
+    indices it serves and its discovered inventory (``GpuInventory.to_dict``)."""
+    from dcos_commons_amd.ops import gpu as G
+
+    inv = G.GpuInventory.from_dict(info["inventory"])
+    return AgentSpec.from_gpu_inventory(info.get("hostname") or f"mi355x-agent-{index}", inv,
+                                        devices=list(info["devices"]), cpus=16, mem=65536, disk=100000)
+
+
 class DeployBench:
     def __init__(self, n_agents: int, profile: str = "mi355x", spec_file: str = "gpu.yml",
                  check_runner: Optional[Callable[[P.TaskInfo, List[int]], bool]] = None,
                  gpu_devices: Optional[List[int]] = None, allocation_interval_s: float = 1.0,
                  timeout_s: float = 120.0, agent_runners: Optional[List[Callable]] = None,
-                 extra_env: Optional[Dict[str, str]] = None):
+                 extra_env: Optional[Dict[str, str]] = None, agent_specs: Optional[List[AgentSpec]] = None,
+                 spec_env: Optional[Dict[str, str]] = None):
         self.n = n_agents
         self.extra_env = dict(extra_env or {})  # scheduler flag overrides on top of the profile
+        self.spec_env = dict(spec_env or {})    # spec rendering overrides (e.g. WORLD_COUNT)
         self.profile = profile
+        # a file of frameworks/helloworld/specs, or an absolute path (the reference's examples)
         self.spec_file = spec_file
         self.check_runner = check_runner
         self.gpu_devices = gpu_devices if gpu_devices is not None else list(range(n_agents))
+        self.agent_specs = agent_specs if agent_specs is not None else agent_specs_from_inventory(self.gpu_devices)
+        if len(self.agent_specs) != n_agents:
+            raise ValueError(f"{len(self.agent_specs)} agent specs for {n_agents} agents")
+        self.last_placement: List[Dict] = []  # LocalMaster.placement() once the last deploy completed
         self.allocation_interval_s = allocation_interval_s
         self.timeout_s = timeout_s
         self.agent_runners = agent_runners  # per-agent check runner (remote GPU agents)
@@ -134,12 +172,8 @@ class DeployBench:
 
     def _make_master(self) -> LocalMaster:
         master = LocalMaster(allocation_interval_s=self.allocation_interval_s, behavior=self.behavior)
-        for i in range(self.n):
-            dev = self.gpu_devices[i % len(self.gpu_devices)]
-            master.add_agent(AgentSpec(hostname=f"mi355x-agent-{i}", cpus=16, mem=65536, disk=100000, gpus=1,
-                                       gpu_devices=[dev],
-                                       attributes={"gpu_vendor": "amd", "gpu_model": "MI355X", "xgmi_hive": "0"}),
-                             check_runner=self.agent_runners[i] if self.agent_runners else None)
+        for i, spec in enumerate(self.agent_specs):
+            master.add_agent(spec, check_runner=self.agent_runners[i] if self.agent_runners else None)
         return master
 
     # -- one cycle -------------------------------------------------------------------------
@@ -147,13 +181,14 @@ class DeployBench:
         ProcessExit.set_test_mode(True)
         t_cycle = time.perf_counter()
         env = helloworld_env(self.n, 1, "amd-gpu-probe --readiness")
+        env.update(self.spec_env)
         overrides = dict(PROFILES[self.profile])
         overrides.update(self.extra_env)
         overrides.update({"PORT_API": "0", "SDK_PERSISTER": "mem"})
         cfg = SchedulerConfig.for_testing(**overrides)
-        path = os.path.join(SPECS, self.spec_file)
+        path = self.spec_file if os.path.isabs(self.spec_file) else os.path.join(SPECS, self.spec_file)
         raw = RawServiceSpec.new_builder(path).set_env(env).build()
-        spec = ServiceSpecGenerator(raw, cfg, SPECS, env).build()
+        spec = ServiceSpecGenerator(raw, cfg, os.path.dirname(path), env).build()
         master = self._make_master()
         builder = SchedulerBuilder(spec, cfg, MemPersister()).set_plans_from(raw)
         marks = {}
@@ -181,6 +216,7 @@ class DeployBench:
             deploy_s = t_done - t0
             deploy_sub = t_done - marks.get("subscribed", t0)
             self._expect_api(router, "deploy")
+            self.last_placement = master.placement()
 
             # failures are injected in steady state: deploy finished and the offer loop has gone
             # idle (suppressed), as for a pod that fails long after its service deployed

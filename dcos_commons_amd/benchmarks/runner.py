@@ -12,7 +12,8 @@ import socket
 import statistics
 import time
 
-from dcos_commons_amd.benchmarks.deploy_bench import DeployBench
+from dcos_commons_amd.benchmarks.deploy_bench import (DeployBench, agent_spec_from_registration,
+                                                      agent_specs_from_inventory, reference_spec)
 
 METRIC = "deploy-plan COMPLETE wall-clock (s) + pod recovery MTTR, helloworld 1/2/4/8 pods"
 
@@ -85,14 +86,62 @@ def _summary(args, n, cycles, elapsed, use_gpu, parallelism):
     }
 
 
+def _reference_row(args, n, make_bench) -> dict:
+    """BASELINE config #5 as the reference itself would run it: its unchanged helloworld
+    ``gpu_resource.yml`` (``gpus: 1`` hello pods, ``hostname:UNIQUE``, no ``plans:`` so the default
+    *serial* deploy of DeployPlanFactory.java:22 / DefaultPhaseFactory.java:35, no readiness
+    check), on the same agents, after the timed region (it does not enter ``value``/``ms_per_step``)."""
+    steps = getattr(args, "reference_steps", 0)
+    path = reference_spec("gpu_resource.yml")
+    if steps <= 0:
+        return {}
+    if path is None:
+        # the repository's rewrite of the same scenario (also no plans: -> serial)
+        path = os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))),
+                            "frameworks", "helloworld", "specs", "gpu_resource.yml")
+        which = "repo frameworks/helloworld/specs/gpu_resource.yml (no reference tree on this machine)"
+    else:
+        which = "reference frameworks/helloworld/src/main/dist/gpu_resource.yml, unchanged"
+    bench = make_bench(path)
+    cycles = [bench.run_cycle() for _ in range(steps)]
+    dep = [c.deploy_s for c in cycles]
+    return {"reference_spec": {
+        "spec": which, "plan": "default serial deploy", "steps": steps, "pods": n,
+        "deploy_s": {"mean": round(statistics.mean(dep), 6), "min": round(min(dep), 6), "max": round(max(dep), 6)},
+        "deploy_from_subscribed_s": {"mean": round(statistics.mean(c.deploy_from_subscribed_s for c in cycles), 6)},
+        "mttr_restart_s": {"mean": round(statistics.mean(c.mttr_restart_s for c in cycles), 6)},
+        "mttr_replace_s": {"mean": round(statistics.mean(c.mttr_replace_s for c in cycles), 6)}}}
+
+
+# the reference example's world pods are not part of BASELINE config #5 (hello pods, one per GPU)
+REFERENCE_ROW_ENV = {"WORLD_COUNT": "0"}
+
+
+def _record(path, payload) -> None:
+    """``SDK_BENCH_RECORD=<dir>``: each rank writes what it saw (tests of the multi-rank path)."""
+    if not path:
+        return
+    import json
+
+    os.makedirs(path, exist_ok=True)
+    with open(os.path.join(path, f"rank{payload.get('rank', 0)}.json"), "w") as f:
+        json.dump(payload, f, indent=1, sort_keys=True)
+
+
 def _run_single(args, n, use_gpu):
     import torch
 
     runner = gpu_check_runner() if use_gpu else None
     ndev = torch.cuda.device_count() if use_gpu else 1
-    bench = DeployBench(n, profile=args.profile, check_runner=runner,
-                        gpu_devices=[i % max(1, ndev) for i in range(n)],
-                        allocation_interval_s=args.allocation_interval, extra_env=_sched_env(args))
+    devices = [i % max(1, ndev) for i in range(n)]
+    # the agents advertise what node discovery finds for their device (ops.gpu)
+    specs = agent_specs_from_inventory(devices)
+
+    def make(spec_file="gpu.yml", spec_env=None):
+        return DeployBench(n, profile=args.profile, check_runner=runner, gpu_devices=devices,
+                           allocation_interval_s=args.allocation_interval, extra_env=_sched_env(args),
+                           agent_specs=specs, spec_file=spec_file, spec_env=spec_env)
+    bench = make()
     for _ in range(args.warmup):
         bench.run_cycle()
     _sync()
@@ -100,7 +149,29 @@ def _run_single(args, n, use_gpu):
     cycles = [bench.run_cycle() for _ in range(args.steps)]
     _sync()
     elapsed = time.perf_counter() - t0
-    return _summary(args, n, cycles, elapsed, use_gpu, f"agents{n}")
+    out = _summary(args, n, cycles, elapsed, use_gpu, f"agents{n}")
+    out["config"]["agent_attributes"] = specs[0].attributes
+    out.update(_reference_row(args, n, lambda path: make(path, REFERENCE_ROW_ENV)))
+    _record(os.environ.get("SDK_BENCH_RECORD"), {"rank": 0, "placement": bench.last_placement,
+                                                 "agents": [_spec_view(s) for s in specs]})
+    return out
+
+
+def _spec_view(spec) -> dict:
+    return {"hostname": spec.hostname, "gpus": spec.gpus, "gpu_devices": list(spec.gpu_devices or []),
+            "attributes": dict(spec.attributes)}
+
+
+def _local_agent_info(rank: int, local_rank: int, device: int) -> dict:
+    """What this rank registers as its agent: a hostname of its own (one agent per GPU, so
+    ``hostname:UNIQUE`` pins pods 1:1), the device it serves, and that device's discovered
+    inventory entry (model, arch, xGMI hive and peers) for the agent's attributes."""
+    from dcos_commons_amd.ops import gpu as G
+
+    inv = G.node_inventory(device + 1)
+    return {"rank": rank, "hostname": f"{socket.gethostname()}-gpu{local_rank}", "devices": [device],
+            "gpus": 1, "inventory": inv.subset([device]).to_dict(),
+            "attributes": inv.subset([device]).attributes()}
 
 
 def _run_distributed(args, rank, world, local_rank, use_gpu, dist):
@@ -116,35 +187,64 @@ def _run_distributed(args, rank, world, local_rank, use_gpu, dist):
                                             master_addr)
         port_box[0] = server.port
     dist.broadcast_object_list(port_box, src=0)
-    n_dev = torch.cuda.device_count() if torch.cuda.is_available() else 1
+    if torch.cuda.is_available():
+        n_dev = torch.cuda.device_count()
+    else:
+        # no GPU (gloo rehearsal / CPU test): the node's discovered (or fixture) devices
+        from dcos_commons_amd.ops import gpu as G
+
+        n_dev = G.node_inventory(1).count
     device = local_rank % max(n_dev, 1)
     local_check = gpu_check_runner() if use_gpu else None
     # collectives run on the GPU under RCCL, on the host under gloo
     coll_dev = "cuda" if torch.cuda.is_available() and getattr(args, "dist_backend", "nccl") == "nccl" else "cpu"
+    record = os.environ.get("SDK_BENCH_RECORD")
+    checks = []  # (devices the master assigned, device the probe ran on, ok)
 
     def check(msg):
-        if local_check is None:
-            return True, "synthetic"
-        ok = local_check(None, [device])
-        return ok, "probe"
+        assigned = list(msg.get("devices") or [device])
+        if assigned != [device]:
+            # the master assigns from the devices this agent registered: anything else is a bug
+            checks.append((assigned, device, False))
+            return False, f"check for devices {assigned} sent to the agent of device {device}"
+        ok = True if local_check is None else local_check(None, [device])
+        checks.append((assigned, device, bool(ok)))
+        return ok, f"{'probe' if local_check is not None else 'synthetic'} on device {device}"
 
+    info = _local_agent_info(rank, local_rank, device)
     if rank != 0:
-        info = {"rank": rank, "hostname": f"{socket.gethostname()}-gpu{local_rank}", "devices": [device]}
-        agent_link.run_agent(master_addr, port_box[0], info, check, on_barrier=lambda: (_sync(), dist.barrier()))
-        # final MAX reduction of the timed region (rank 0 drives it)
-        t = torch.zeros(1, dtype=torch.float64, device=coll_dev)
+        marks = []
+
+        def on_barrier():
+            _sync()
+            dist.barrier()
+            marks.append(time.perf_counter())
+        agent_link.run_agent(master_addr, port_box[0], info, check, on_barrier=on_barrier)
+        # this rank's view of the timed region (between rank 0's two barriers), MAX-reduced with
+        # every other rank's
+        elapsed = marks[-1] - marks[0] if len(marks) >= 2 else 0.0
+        t = torch.tensor([elapsed], dtype=torch.float64, device=coll_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        _record(record, {"rank": rank, "device": device, "registered": info, "checks": checks,
+                         "elapsed_local_s": elapsed, "elapsed_max_s": float(t.item())})
         return {}
 
     remotes = server.wait_for(world - 1)
 
     def local_runner(task_info, devices):
-        return check({})[0]
+        return check({"devices": devices})[0]
     local_runner.inline = True   # the local probe (or the synthetic pass) is one short call
 
     runners = [local_runner] + [agent_link.RemoteCheckRunner(r) for r in remotes]
-    bench = DeployBench(world, profile=args.profile, agent_runners=runners, gpu_devices=list(range(world)),
-                        allocation_interval_s=args.allocation_interval, extra_env=_sched_env(args))
+    # every agent is what its rank registered: hostname, device, discovered attributes
+    specs = [agent_spec_from_registration(info, 0)] + [agent_spec_from_registration(r.info, i + 1)
+                                                       for i, r in enumerate(remotes)]
+
+    def make(spec_file="gpu.yml", spec_env=None):
+        return DeployBench(world, profile=args.profile, agent_runners=runners, agent_specs=specs,
+                           allocation_interval_s=args.allocation_interval, extra_env=_sched_env(args),
+                           spec_file=spec_file, spec_env=spec_env)
+    bench = make()
     for _ in range(args.warmup):
         bench.run_cycle()
 
@@ -159,7 +259,15 @@ def _run_distributed(args, rank, world, local_rank, use_gpu, dist):
     _sync()
     barrier()
     elapsed = time.perf_counter() - t0
+    placement = bench.last_placement
+    extra = _reference_row(args, world, lambda path: make(path, REFERENCE_ROW_ENV))
     server.close()
     t = torch.tensor([elapsed], dtype=torch.float64, device=coll_dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    return _summary(args, world, cycles, float(t.item()), use_gpu, f"agents{world}-ranks{world}")
+    _record(record, {"rank": 0, "device": device, "registered": info, "checks": checks, "placement": placement,
+                     "agents": [_spec_view(s) for s in specs], "elapsed_local_s": elapsed,
+                     "elapsed_max_s": float(t.item())})
+    out = _summary(args, world, cycles, float(t.item()), use_gpu, f"agents{world}-ranks{world}")
+    out["config"]["agent_attributes"] = specs[0].attributes
+    out.update(extra)
+    return out

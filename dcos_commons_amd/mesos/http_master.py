@@ -31,7 +31,7 @@ from dcos_commons_amd.mesos import protos as P
 from dcos_commons_amd.mesos import recordio
 from dcos_commons_amd.mesos.http_driver import JSON, PROTOBUF, SCHEDULER_PATH, STREAM_ID_HEADER, decode_message, \
     encode_message
-from dcos_commons_amd.mesos.local_master import AgentSpec, LocalMaster, TERMINAL
+from dcos_commons_amd.mesos.local_master import TERMINAL, LocalMaster, gpu_agent_specs
 from dcos_commons_amd.utils.http_server import QuietThreadingHTTPServer
 
 LOGGER = logging.getLogger(__name__)
@@ -377,16 +377,16 @@ def main(argv=None) -> int:
     ap.add_argument("--cpus", type=float, default=8.0)
     ap.add_argument("--mem", type=float, default=32768.0)
     ap.add_argument("--disk", type=float, default=65536.0)
-    ap.add_argument("--gpus", type=int, default=0)
+    ap.add_argument("--gpus", default="0",
+                    help="GPUs per agent, or 'auto' to split this node's discovered GPUs between the agents")
     ap.add_argument("--allocation-interval", type=float, default=1.0)
     ap.add_argument("--heartbeat", type=float, default=15.0)
     args = ap.parse_args(argv)
     logging.basicConfig(level=logging.INFO, format="%(asctime)s %(levelname)s %(name)s: %(message)s")
     lm = LocalMaster(allocation_interval_s=args.allocation_interval)
-    for i in range(args.agents):
-        attrs = {"gpu_vendor": "amd", "gpu_model": "MI355X"} if args.gpus else {}
-        lm.add_agent(AgentSpec(hostname=f"agent-{i}.local", cpus=args.cpus, mem=args.mem, disk=args.disk,
-                               gpus=args.gpus, attributes=attrs))
+    for spec in gpu_agent_specs(args.agents, args.gpus if args.gpus == "auto" else int(args.gpus),
+                                lambda i: f"agent-{i}.local", cpus=args.cpus, mem=args.mem, disk=args.disk):
+        lm.add_agent(spec)
     hm = HttpMaster(lm, args.host, args.port, heartbeat_s=args.heartbeat).start()
     print(f"master listening on {hm.url}", flush=True)
     try:

@@ -46,6 +46,7 @@ from dcos_commons_amd.mesos.resource_math import (
     strip_volume,
 )
 from dcos_commons_amd import trace
+from dcos_commons_amd.ops.gpu import select_devices
 from dcos_commons_amd.utils import ids
 
 LOGGER = logging.getLogger(__name__)
@@ -87,6 +88,23 @@ class AgentSpec:
     region: Optional[str] = None
     mount_disks: Tuple[tuple, ...] = ()  # (root, size) or (root, size, profile)
     pre_reserved: Tuple[Tuple[str, str, float], ...] = ()  # (role, resource name, amount)
+    # device index -> xGMI hive id / direct xGMI peers (``ops.gpu`` discovery): a ``gpus: N`` task
+    # gets N devices of one hive when the agent has them free (``ops.gpu.select_devices``)
+    gpu_hives: Optional[Dict[int, str]] = None
+    gpu_peers: Optional[Dict[int, Tuple[int, ...]]] = None
+
+    @staticmethod
+    def from_gpu_inventory(hostname: str, inventory, devices: Optional[List[int]] = None,
+                           attributes: Optional[Dict[str, str]] = None, **kw) -> "AgentSpec":
+        """An agent owning ``devices`` (default: all) of a discovered ``ops.gpu.GpuInventory``:
+        ``gpus`` is their count, ``gpu_devices`` their indices, and the agent's attributes carry
+        their vendor / model / arch / xGMI hive (``GpuInventory.attributes``)."""
+        inv = inventory if devices is None else inventory.subset(devices)
+        attrs = dict(inv.attributes())
+        attrs.update(attributes or {})
+        return AgentSpec(hostname=hostname, gpus=inv.count, gpu_devices=[d.index for d in inv.devices],
+                         attributes=attrs, gpu_hives=inv.hive_map(),
+                         gpu_peers={d.index: tuple(d.xgmi_peers) for d in inv.devices}, **kw)
 
     def resources(self) -> List[P.Resource]:
         out = []
@@ -504,6 +522,19 @@ class LocalMaster:
             return out
         return self.call(do)
 
+    def placement(self) -> List[Dict]:
+        """Where every live task runs: task name, agent hostname and attributes, and the GPU
+        devices the agent assigned it (what ``HIP_VISIBLE_DEVICES`` carries)."""
+        def do():
+            out = []
+            for a in self.agents.values():
+                for t in a.tasks.values():
+                    if t.status.state not in TERMINAL:
+                        out.append({"task": t.info.name, "hostname": a.spec.hostname,
+                                    "attributes": dict(a.spec.attributes), "gpu_devices": list(t.gpu_devices)})
+            return sorted(out, key=lambda x: x["task"])
+        return self.call(do)
+
     def agent_resources(self, agent_id: str) -> List[P.Resource]:
         return self.call(lambda: self.agents[agent_id].available.to_resources())
 
@@ -854,7 +885,8 @@ class LocalMaster:
         if new_exec:
             agent.executors[key] = _Executor(executor, fw.id, exec_rs)
         for t, rs, ng in zip(tasks, per_task, gpus_needed):
-            devices = [agent.free_gpus.pop(0) for _ in range(ng)]
+            devices = select_devices(agent.free_gpus, ng, agent.spec.gpu_hives, agent.spec.gpu_peers)
+            agent.free_gpus = [d for d in agent.free_gpus if d not in devices]
             st = P.TaskStatus(state=P.TASK_STAGING, source=P.TaskStatus.SOURCE_MASTER, timestamp=time.time())
             st.task_id.CopyFrom(t.task_id)
             st.agent_id.value = agent.id
@@ -1208,13 +1240,43 @@ class LocalSchedulerDriver(SchedulerDriver):
 def local_master_from_env(env) -> LocalMaster:
     """An in-process cluster sized from ``SDK_LOCAL_*`` variables (``SDK_MESOS_MASTER=local``)."""
     n = env.get_optional_int("SDK_LOCAL_AGENTS", 3)
-    gpus = env.get_optional_int("SDK_LOCAL_AGENT_GPUS", 0)
+    gpus_env = env.get_optional("SDK_LOCAL_AGENT_GPUS", "0")
     master = LocalMaster(allocation_interval_s=env.get_optional_double("SDK_LOCAL_ALLOCATION_INTERVAL_S", 1.0))
-    for i in range(n):
-        attrs = {"gpu_vendor": "amd", "gpu_model": "MI355X"} if gpus else {}
-        master.add_agent(AgentSpec(hostname=f"agent-{i}.local",
-                                   cpus=env.get_optional_double("SDK_LOCAL_AGENT_CPUS", 8.0),
-                                   mem=env.get_optional_double("SDK_LOCAL_AGENT_MEM", 32768.0),
-                                   disk=env.get_optional_double("SDK_LOCAL_AGENT_DISK", 65536.0),
-                                   gpus=gpus, attributes=attrs))
+    specs = gpu_agent_specs(n, gpus_env, lambda i: f"agent-{i}.local")
+    for spec in specs:
+        spec.cpus = env.get_optional_double("SDK_LOCAL_AGENT_CPUS", 8.0)
+        spec.mem = env.get_optional_double("SDK_LOCAL_AGENT_MEM", 32768.0)
+        spec.disk = env.get_optional_double("SDK_LOCAL_AGENT_DISK", 65536.0)
+        master.add_agent(spec)
     return master
+
+
+def gpu_agent_specs(agents: int, gpus_per_agent, hostname, inventory=None, **kw) -> List[AgentSpec]:
+    """``agents`` GPU agent specs built from node discovery (``ops.gpu``).
+
+    ``gpus_per_agent="auto"``: the agents share this one node and split its discovered GPUs in
+    contiguous blocks (one agent per GPU on an 8-GPU node). An int: every agent stands for a node
+    of its own with that many GPUs (a simulated cluster): the first ones of this node's inventory,
+    or of ``inventory``. Each agent's ``gpu_devices``, attributes (``gpu_model``, ``xgmi_hive``,
+    ...) and device topology come from the inventory; a node with fewer GPUs than asked for (no
+    driver here) gets a synthetic MI355X inventory of the right size."""
+    from dcos_commons_amd.ops import gpu as G
+
+    if gpus_per_agent == "auto":
+        inv = inventory if inventory is not None else G.node_inventory()
+        per = inv.count // agents if agents else 0
+        blocks = [[d.index for d in inv.devices[i * per:(i + 1) * per]] for i in range(agents)]
+    else:
+        per = int(gpus_per_agent or 0)
+        inv = inventory if inventory is not None else (G.node_inventory(per) if per else None)
+        if per and inv.count < per:
+            raise ValueError(f"{per} GPUs per agent, the inventory has {inv.count}")
+        blocks = [[d.index for d in inv.devices[:per]] for _ in range(agents)] if per else []
+    out = []
+    for i in range(agents):
+        name = hostname(i) if callable(hostname) else f"{hostname}-{i}"
+        if per:
+            out.append(AgentSpec.from_gpu_inventory(name, inv, devices=blocks[i], **kw))
+        else:
+            out.append(AgentSpec(hostname=name, **kw))
+    return out

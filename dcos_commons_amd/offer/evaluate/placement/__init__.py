@@ -4,8 +4,8 @@ Reference: sdk/.../offer/evaluate/placement/*.java (38 files, 3.3K LoC). Every r
 ``filter(offer, pod_instance, tasks) -> EvaluationOutcome`` and serializes with the Jackson
 ``@type`` discriminator (PlacementRule.java:24) so persisted ServiceSpecs keep their rules.
 
-MI355X note: agents advertise ``gpu_vendor``/``gpu_model``/``xgmi_hive`` attributes (see
-``dcos_commons_amd.ops.gpu``), so ``[["xgmi_hive","GROUP_BY"]]`` or
+MI355X note: agents advertise ``gpu_vendor``/``gpu_model``/``gpu_arch``/``xgmi_hive`` attributes (see
+``dcos_commons_amd.ops.gpu``: KFD topology / amd-smi discovery), so ``[["xgmi_hive","GROUP_BY","2"]]`` or
 ``[["hostname","MAX_PER","1"]]`` give topology-aware 1:1 GPU pinning with no special rule.
 """
 from __future__ import annotations

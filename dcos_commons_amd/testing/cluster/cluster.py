@@ -31,7 +31,8 @@ from typing import Dict, Iterable, List, Optional, Sequence
 
 from dcos_commons_amd.mesos import protos as P
 from dcos_commons_amd.mesos.http_master import HttpMaster
-from dcos_commons_amd.mesos.local_master import TERMINAL, AgentSpec, LocalMaster, TaskBehavior, TaskTiming
+from dcos_commons_amd.mesos.local_master import (TERMINAL, AgentSpec, LocalMaster, TaskBehavior, TaskTiming,
+                                                  gpu_agent_specs)
 from dcos_commons_amd.testing.cluster.marathon import LocalMarathon
 from dcos_commons_amd.testing.cluster.packages import LocalCosmos
 from dcos_commons_amd.testing.zk_server import ZkServer
@@ -149,7 +150,7 @@ class LocalCluster:
                  packages: Optional[Dict[str, str]] = None, scheduler_env: Optional[Dict[str, str]] = None,
                  finish_tasks: Sequence[str] = (), dcos_version: str = "1.13.0", keep_work_dir: bool = False,
                  mount_disks: Sequence[tuple] = (), dcos_security: bool = False, zk_process: bool = False,
-                 gpu_probe_service: bool = False):
+                 gpu_probe_service: bool = False, gpu_inventory=None):
         self.work_dir = os.path.abspath(work_dir or tempfile.mkdtemp(prefix="sdk-cluster-"))
         self._own_work_dir = work_dir is None and not keep_work_dir
         self.region = region
@@ -185,13 +186,13 @@ class LocalCluster:
             raise ValueError(f"executor must be 'process' or 'synthetic', not {executor!r}")
         self.executor = executor
         if agent_specs is None:
-            agent_specs = [AgentSpec(hostname=f"10.0.0.{i + 1}", cpus=agent_cpus, mem=agent_mem, disk=agent_disk,
-                                     ports=DCOS_AGENT_PORTS,
-                                     region=region, zone=zones[i % len(zones)] if zones else None,
-                                     gpus=gpus_per_agent, mount_disks=tuple(mount_disks),
-                                     attributes=({"gpu_vendor": "amd", "gpu_model": "MI355X"}
-                                                 if gpus_per_agent else {}))
-                           for i in range(agents)]
+            # GPU agents split this node's discovered GPUs (ops.gpu: KFD topology / amd-smi), with
+            # their model and xGMI hive as attributes; a driverless node gets synthetic MI355X ones
+            agent_specs = gpu_agent_specs(agents, gpus_per_agent, lambda i: f"10.0.0.{i + 1}", inventory=gpu_inventory,
+                                          cpus=agent_cpus, mem=agent_mem, disk=agent_disk, ports=DCOS_AGENT_PORTS,
+                                          region=region, mount_disks=tuple(mount_disks))
+            for i, spec in enumerate(agent_specs):
+                spec.zone = zones[i % len(zones)] if zones else None
         self._agent_specs = list(agent_specs)
         domain = P.DomainInfo()
         domain.fault_domain.region.name = region

@@ -52,6 +52,57 @@ def test_bench_single_process():
     _check(recs[0], 1, 1, 0)
 
 
+@pytest.mark.timeout(400)
+def test_bench_four_ranks_build_agents_from_what_each_rank_registers(tmp_path):
+    """The driver's N-GPU run, rehearsed on CPU: 4 ranks over gloo, each discovering "its" GPU
+    from a recorded-format KFD tree of a 4-GPU node in two xGMI hives (``ops.gpu``). Checks that
+    the offers came from each rank's registration (hostname, device, model, hive), every
+    readiness check ran on the registering rank's own device, and the JSON reports n_gpus=4 with
+    the time MAX-reduced over the ranks."""
+    from dcos_commons_amd.ops import gpu as G
+
+    fixture = tmp_path / "node"
+    G.synthetic_kfd_tree(str(fixture / "kfd"), [0xA1, 0xA1, 0xB2, 0xB2])
+    record = tmp_path / "record"
+    env = dict(os.environ, PYTHONPATH=ROOT, MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="1",
+               SDK_GPU_DISCOVERY_FIXTURE=str(fixture), SDK_BENCH_RECORD=str(record))
+    env.pop("CUDA_VISIBLE_DEVICES", None)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "4",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(ROOT, "bench.py"), "--gpus", "4", "--steps", "2", "--warmup", "1", "--no-gpu-probe",
+           "--allocation-interval", "0.05", "--reference-steps", "1"]
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=380, env=env, cwd=ROOT)
+    assert p.returncode == 0, p.stderr[-3000:]
+    recs = _json_lines(p.stdout)
+    assert len(recs) == 1, p.stdout
+    rec = recs[0]
+    _check(rec, 4, 2, 1)
+    assert rec["config"]["parallelism"] == "agents4-ranks4"
+    assert rec["reference_spec"]["pods"] == 4 and rec["reference_spec"]["plan"] == "default serial deploy"
+    ranks = {r: json.load(open(record / f"rank{r}.json")) for r in range(4)}
+    hive = {0: "a1", 1: "a1", 2: "b2", 3: "b2"}
+    for r, data in ranks.items():
+        assert data["device"] == r and data["registered"]["devices"] == [r]
+        assert data["registered"]["attributes"]["xgmi_hive"] == hive[r]
+        # every check this rank served was for its own device, and ran there
+        assert data["checks"] and all(a == [r] and d == r and ok for a, d, ok in data["checks"])
+    # the agents rank 0 offered are exactly what the ranks registered
+    agents = {a["hostname"]: a for a in ranks[0]["agents"]}
+    for r, data in ranks.items():
+        a = agents[data["registered"]["hostname"]]
+        assert a["gpu_devices"] == [r] and a["attributes"]["xgmi_hive"] == hive[r]
+        assert a["attributes"]["gpu_model"] == "MI355X" and a["attributes"]["gpu_arch"] == "gfx950"
+    # one hello pod per agent (hostname:UNIQUE), each on that agent's device
+    placed = {x["hostname"]: x for x in ranks[0]["placement"] if x["task"].startswith("hello-")}
+    assert len(placed) == 4
+    for host, x in placed.items():
+        assert x["gpu_devices"] == agents[host]["gpu_devices"]
+    # the reported time is the MAX over the ranks' own views of the timed window
+    elapsed = [d["elapsed_local_s"] for d in ranks.values()]
+    assert all(d["elapsed_max_s"] == max(elapsed) for d in ranks.values())
+    assert abs(rec["ms_per_step"] - max(elapsed) * 1000 / 2) < 0.01
+
+
 @pytest.mark.timeout(300)
 def test_bench_two_ranks_over_gloo():
     env = dict(os.environ, PYTHONPATH=ROOT, MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="1")
