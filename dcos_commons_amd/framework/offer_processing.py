@@ -443,6 +443,7 @@ class OfferProcessor:
         self.accepter = OfferAccepter()
         self.multithreaded = True
         self.hold_s = hold_s
+        self._declined_long_in_cycle = False  # some offer of the running cycle was declined for an hour
         self.event_driven = event_driven
         # reference: stale reservations are only collected from offers nothing was launched on,
         # and only while the service is WORKING (OfferProcessor.java:300-330), so a pod replaced
@@ -591,6 +592,7 @@ class OfferProcessor:
         # released reservations: the REVIVE goes out before the cycle, so the master allocates them
         # while the cycle runs instead of after it
         revived_early = reoffer and self._reoffer_revive()
+        self._declined_long_in_cycle = False
         now = time.monotonic()
         with self._held_lock:
             held = [o for o, _ in self._held.values()]
@@ -630,9 +632,12 @@ class OfferProcessor:
                     if self.gc_all_offers:
                         offers = self._collect_garbage(offers)
                     decline_long(offers)
-            if revived_early:
+                    self._declined_long_in_cycle = True
+            if revived_early and (self.hold_s > 0 or not self._declined_long_in_cycle):
                 # the master has allocated everything available since that REVIVE: a revive this
-                # cycle asked for (new work) would only repeat it
+                # cycle asked for (new work) would only repeat it. Not when this cycle declined
+                # offers for an hour (hold_s == 0): only a REVIVE issued after that decline clears
+                # its filters, so the cycle's own work-set revive must still go out
                 self.revive_manager.cancel_request()
             elif reoffer:
                 # throttled before the cycle: requested again after the cycle's own revive
@@ -757,6 +762,7 @@ class OfferProcessor:
                     to_decline_short = unused
         decline_short(to_decline_short)
         decline_long(to_decline_long)
+        self._declined_long_in_cycle = self._declined_long_in_cycle or bool(to_decline_long)
         if resp.streamed:
             all_recs = [r for r in pre_cleanup if id(r) not in streamed_pre] + cleanup_recs
         else:

@@ -238,6 +238,23 @@ class _Agent:
         self.check_runner = None  # per-agent check executor (e.g. a remote GPU agent)
         self.index = 0            # position among the master's agents (overlay subnet 9.0.<index>.0/24)
         self._overlay_ips = itertools.count(2)
+        self._check_thread = None  # the agent's own thread for inline checks (see check_thread)
+
+    def check_thread(self):
+        """This agent's check executor: one thread, as a Mesos agent's executor runs its tasks'
+        checks. Inline checks (one short native call, e.g. the fused HIP probe) run here, never on
+        the master's event thread: a slow or hung probe on one GPU stalls only its own agent, and
+        the checks of different agents' GPUs run in parallel."""
+        if self._check_thread is None:
+            from concurrent.futures import ThreadPoolExecutor
+
+            self._check_thread = ThreadPoolExecutor(max_workers=1, thread_name_prefix=f"check-{self.spec.hostname}")
+            self._check_thread.submit(lambda: None).result(10)   # started before any task launches
+        return self._check_thread
+
+    def close(self) -> None:
+        if self._check_thread is not None:
+            self._check_thread.shutdown(wait=False)
 
     @property
     def ip(self) -> str:
@@ -381,6 +398,8 @@ class LocalMaster:
             self._cond.notify_all()
         if threading.current_thread() is not self._thread:
             self._thread.join(timeout=5)
+        for a in list(self.agents.values()):
+            a.close()
         stop = getattr(self.behavior, "shutdown", None)
         if callable(stop):
             stop()
@@ -397,7 +416,11 @@ class LocalMaster:
             self.agents[aid].index = len(self.agents)
             self._allocate()
             return aid
-        return self.call(do)
+        aid = self.call(do)
+        runner = check_runner if check_runner is not None else self.behavior.check_runner
+        if getattr(runner, "inline", False):
+            self.agents[aid].check_thread()   # started now, outside any timed launch
+        return aid
 
     def add_mount_disks(self, agent_id: str, disks) -> None:
         """Attach MOUNT disks (``(root, size[, profile])``) to a registered agent, as an agent
@@ -967,11 +990,12 @@ class LocalMaster:
                 LOGGER.exception("check of %s raised", task.info.name)
                 return False
 
-        if getattr(runner, "inline", False):
+        agent = self.agents.get(task.agent_id)
+        if getattr(runner, "inline", False) and agent is not None:
             # a check that is one short native call (the fused HIP probe, ~0.07 ms with the
-            # interpreter released) runs on the agent's own thread, as an executor runs its
-            # checks: a pool thread would add two thread hand-offs to a pod's readiness
-            self._check_result(task, epoch, check())
+            # interpreter released) runs on the agent's own check thread (not on this
+            # event thread, where a slow probe would stall every agent's launches and statuses)
+            agent.check_thread().submit(lambda: self._schedule(0, self._check_result, task, epoch, check()))
             return
         self.behavior.pool().submit(lambda: self._schedule(0, self._check_result, task, epoch, check()))
 

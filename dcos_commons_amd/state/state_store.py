@@ -159,18 +159,31 @@ class StateStore:
     def store_status(self, task_name: str, status: P.TaskStatus,
                      properties: Optional[Dict[str, bytes]] = None) -> None:
         """Stores ``status`` (StateStore.storeStatus). ``properties`` are written in the same
-        persister transaction (one ZooKeeper multi instead of a round trip each)."""
+        persister transaction (one ZooKeeper multi instead of a round trip each), but never at the
+        status's expense: the reference stores them after the status in a try/catch that only
+        warns (DefaultScheduler.java:541-560, StateStoreUtils.storeTaskStatusAsProperty), so a
+        property that fails validation is dropped with a warning, and a combined write that fails
+        is retried as the status alone."""
         self._check_status(task_name, status)
+        data = status.SerializeToString()
+        valid: Dict[str, bytes] = {}
+        for k, v in (properties or {}).items():
+            try:
+                self._validate_key(k)
+                self._validate_value(v)
+            except StateStoreException as e:
+                self.logger.warning("Not storing property '%s' with the status of %s: %s", k, task_name, e)
+                continue
+            valid[self._property_path(k)] = v
         try:
-            if properties:
-                m = {self._task_status_path(task_name): status.SerializeToString()}
-                for k, v in properties.items():
-                    self._validate_key(k)
-                    self._validate_value(v)
-                    m[self._property_path(k)] = v
-                self.persister.set_many(m)
-            else:
-                self.persister.set(self._task_status_path(task_name), status.SerializeToString())
+            if valid:
+                try:
+                    self.persister.set_many(dict(valid, **{self._task_status_path(task_name): data}))
+                    return
+                except PersisterException as e:
+                    self.logger.warning("Failed to store properties %s with the status of %s (%s); "
+                                        "storing the status alone", sorted(valid), task_name, e)
+            self.persister.set(self._task_status_path(task_name), data)
         except PersisterException as e:
             raise StateStoreException(e.reason, str(e)) from e
 

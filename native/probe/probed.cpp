@@ -217,7 +217,9 @@ int main(int argc, char** argv) {
       const int cfd = ::accept4(lfd, nullptr, nullptr, SOCK_CLOEXEC);
       if (cfd >= 0 && g_inflight.load() >= MAX_INFLIGHT) {
         // more concurrent checks than a node has GPUs many times over: refuse rather than spawn
-        // without bound (the check fails and the agent retries it at its next interval)
+        // without bound. amd-gpu-ready asks once more after a short backoff, then fails the check
+        // (exit 1) so the agent retries it at its next interval -- it does not start a standalone
+        // HIP runtime while the node is saturated.
         write_all(cfd, "{\"error\": \"busy\"}\n");
         ::close(cfd);
       } else if (cfd >= 0) {
@@ -236,5 +238,13 @@ int main(int argc, char** argv) {
   // probes in flight finish (their kernels drain) before the process exits
   const long long deadline = now_ms() + 10000;
   while (g_inflight.load() > 0 && now_ms() < deadline) std::this_thread::sleep_for(std::chrono::milliseconds(5));
+  const int left = g_inflight.load();
+  if (left > 0) {
+    // detached connection threads are still inside amdprobe_readiness: running static destructors
+    // and the HIP runtime's teardown under them could crash at exit, so leave without either
+    std::fprintf(stderr, "amd-gpu-probed: %d probe(s) still in flight after 10 s; exiting without teardown\n", left);
+    std::fflush(stderr);
+    std::_Exit(3);
+  }
   return 0;
 }

@@ -132,7 +132,21 @@ int main(int argc, char** argv) {
   if (device < 0) return usage();
   const int physical = physical_device(device);
   std::string reply;
-  if (physical >= 0 && ask(path, physical, inject, reply)) {
+  bool reached = physical >= 0 && ask(path, physical, inject, reply);
+  if (reached && reply.find("\"busy\"") != std::string::npos) {
+    // the service is saturated (its in-flight cap): ask once more after a short backoff. A
+    // standalone probe here would start a whole HIP runtime of its own (0.3-0.4 s) exactly when
+    // the node is busiest, so a second refusal fails the check and the agent retries it at the
+    // check's next interval.
+    ::usleep(20 * 1000);
+    reply.clear();
+    reached = ask(path, physical, inject, reply);
+    if (reached && reply.find("\"busy\"") != std::string::npos) {
+      std::fprintf(stderr, "amd-gpu-ready: probe service busy; check fails, retried at the next interval\n");
+      return 1;
+    }
+  }
+  if (reached) {
     if (reply.find("\"error\"") == std::string::npos) {
       if (json) std::fputs(reply.c_str(), stdout);
       return reply.find("\"healthy\": true") != std::string::npos ? 0 : 1;

@@ -869,3 +869,22 @@ def test_multi_service_offer_cycle_useful_is_any_service():
     assert c.offer_cycle_useful()
     c.manager = M([S(False), object()])               # a service without the predicate: always
     assert c.offer_cycle_useful()
+
+
+@pytest.mark.parametrize("hold_s", [0.0, 10.0])
+def test_early_reoffer_revive_keeps_the_work_set_revive_after_a_long_decline(drv, hold_s):
+    """a cycle that starts with the re-offer REVIVE (released reservations) and finds
+    new work asks for a revive of its own. With held offers (hold_s > 0) that second revive would
+    only repeat the first. With hold_s == 0 the cycle declines its leftovers for an hour, and only
+    a REVIVE issued after that decline clears those filters, so it must not be cancelled."""
+    c = Client(status=ClientStatusResponse.launching(True))
+    p = processor(c, hold_s=hold_s, event_driven=True).disable_threading()
+    p.start()
+    p.reoffer_released()
+    p.enqueue([offer("a")])
+    if hold_s == 0:
+        assert drv.declines == [(["a"], 3600)]
+        # the work-set revive survives the cycle: sent now or, when the spacing holds it, pending
+        assert drv.revives == 2 or (drv.revives == 1 and p.revive_manager.revive_requested)
+    else:
+        assert drv.declines == [] and drv.revives == 1 and not p.revive_manager.revive_requested

@@ -41,3 +41,46 @@ def test_quiet_http_server_drops_client_disconnects_only(caplog):
     finally:
         srv.shutdown()
         srv.server_close()
+
+
+def test_api_server_stops_at_once_and_frees_its_port():
+    """Scheduler restarts (failover, config rollout) stop the API server: the serve loop is woken
+    by a stop pipe, not by socketserver's poll interval (was ~170 ms of every stop)."""
+    from dcos_commons_amd.http.server import ApiServer
+    from dcos_commons_amd.scheduler.scheduler_config import SchedulerConfig
+
+    started = threading.Event()
+    srv = ApiServer.start(SchedulerConfig.for_testing(PORT_API="0"), [], started.set, port=0)
+    assert started.wait(5)
+    with urllib.request.urlopen(f"http://127.0.0.1:{srv.port}/v1/metrics", timeout=5) as r:
+        assert r.status == 200
+    t0 = time.perf_counter()
+    srv.stop()
+    assert time.perf_counter() - t0 < 0.05
+    srv._thread.join(1)
+    assert not srv._thread.is_alive()
+    s = socket.socket()
+    try:
+        s.settimeout(1)
+        assert s.connect_ex(("127.0.0.1", srv.port)) != 0
+    finally:
+        s.close()
+
+
+def test_scheduler_runner_stop_is_bounded():
+    from dcos_commons_amd.benchmarks.deploy_bench import DeployBench
+    from dcos_commons_amd.scheduler.scheduler_runner import SchedulerRunner
+
+    stops = []
+    orig = SchedulerRunner.stop
+
+    def timed(self):
+        t0 = time.perf_counter()
+        orig(self)
+        stops.append(time.perf_counter() - t0)
+    SchedulerRunner.stop = timed
+    try:
+        DeployBench(1, allocation_interval_s=0.05).run_cycle()
+    finally:
+        SchedulerRunner.stop = orig
+    assert stops and max(stops) < 0.05, stops

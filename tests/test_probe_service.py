@@ -129,6 +129,34 @@ def test_client_exit_codes(client, tmp_path):
     assert r.returncode == 2
 
 
+def test_client_busy_service_retries_once_then_fails_without_a_standalone_probe(client, tmp_path):
+    """a saturated service answers ``busy``; the client asks once more after a short
+    backoff and then fails the check (exit 1: the agent retries at the next interval). It does not
+    start ``amd-gpu-probe`` -- a fresh HIP runtime per refused check would add load exactly when
+    the node is busiest."""
+    exe, env = client
+    healthy = json.dumps({"device": 0, "healthy": True})
+    mode = {"busy": 2}
+
+    def reply(line):
+        if mode["busy"] > 0:
+            mode["busy"] -= 1
+            return json.dumps({"error": "busy"})
+        return healthy
+    svc = FakeService(str(tmp_path / "s.sock"), reply)
+    try:
+        # busy twice: exit 1, exactly two requests, no fallback message
+        r = _run(exe, env, "--socket", svc.path)
+        assert r.returncode == 1 and len(svc.requests) == 2, (r.returncode, svc.requests, r.stderr)
+        assert "busy" in r.stderr and "standalone" not in r.stderr
+        # busy once: the retry gets the answer
+        mode["busy"] = 1
+        r = _run(exe, env, "--socket", svc.path)
+        assert r.returncode == 0 and len(svc.requests) == 4
+    finally:
+        svc.close()
+
+
 def test_client_falls_back_to_the_standalone_probe(client, tmp_path):
     """Without a service the check runs ``amd-gpu-probe --readiness`` next to it as a child: on a
     host without a GPU that probe reports unhealthy (1), so the check fails rather than passing."""

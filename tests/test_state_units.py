@@ -361,3 +361,32 @@ def test_schema_version_store(persister):
     persister.set("SchemaVersion", b"not-a-number")
     with pytest.raises(Exception):
         SchemaVersionStore(persister).check(SchemaVersion.SINGLE_SERVICE)
+
+
+def test_status_is_stored_even_when_its_property_is_not(store, persister):
+    """the ``<task>:task-status`` property rides in the status's transaction, but as in
+    the reference (stored after the status, failures only logged) it can never cost the status."""
+    t = info()
+    store.store_tasks([t])
+    st = status(t.task_id)
+    # an invalid key or an oversized value: dropped with a warning, the status is stored
+    store.store_status(TASK, st, {"bad/key": b"v", TASK + ":task-status": b"x" * (1024 * 1024 + 1)})
+    assert store.fetch_status(TASK) == st
+    assert store.fetch_property_keys() == []
+    # a valid property is written with it
+    store.store_status(TASK, st, {TASK + ":task-status": st.SerializeToString()})
+    assert store.fetch_property(TASK + ":task-status") == st.SerializeToString()
+
+    # the combined write failing: the status alone is retried
+    class Flaky(MemPersister):
+        def set_many(self, values):
+            from dcos_commons_amd.storage.persister import PersisterException
+
+            if any("Properties" in k for k in values):
+                raise PersisterException(Reason.STORAGE_ERROR, "multi failed")
+            return super().set_many(values)
+    flaky = StateStore(Flaky())
+    flaky.store_tasks([t])
+    st2 = status(t.task_id, P.TASK_FAILED)
+    flaky.store_status(TASK, st2, {TASK + ":task-status": st2.SerializeToString()})
+    assert flaky.fetch_status(TASK) == st2
