@@ -5,6 +5,7 @@
 * ``native/build/amd-gpu-probed``      -- node-local readiness service (keeps the HIP runtime and the
   per-device probe contexts resident; ``amd-gpu-ready``, a CMake target, is its client);
 * ``native/build/sdk-bootstrap``, ``native/build/sdk-cli`` -- C++ task bootstrap and service CLI.
+* ``native/build/keytab-fix`` -- hdfs keytab rewriter run by Kerberized hdfs tasks (HADOOP-16283).
 
 Everything is compiled directly with ``hipcc --offload-arch=gfx950`` / ``g++`` (no hipify, no
 JIT cache outside the tree) so the built files travel with the repository snapshot.
@@ -85,7 +86,7 @@ def build_cpp_tools(force: bool = False, verbose: bool = False, sanitize: bool =
         return []
     out = BUILD_SANITIZE if sanitize else BUILD
     os.makedirs(out, exist_ok=True)
-    names = ("sdk-bootstrap", "sdk-cli", "native-tests", "tls-tests", "amd-gpu-ready") + (
+    names = ("sdk-bootstrap", "sdk-cli", "native-tests", "tls-tests", "amd-gpu-ready", "keytab-fix") + (
         () if sanitize else ("libsdktls.so",))
     targets = [os.path.join(out, n) for n in names]
     srcs = []

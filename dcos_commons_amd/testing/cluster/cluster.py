@@ -303,15 +303,18 @@ class LocalCluster:
         return value.encode("utf-8") if isinstance(value, str) else value
 
     def _stage_native_artifacts(self) -> None:
-        """``bootstrap.zip`` (every SDK task fetches it) holds this tree's native ``sdk-bootstrap``."""
+        """``bootstrap.zip`` (every SDK task fetches it) holds this tree's native ``sdk-bootstrap``;
+        ``keytab-fix.tar.gz`` (Kerberized hdfs tasks) its native ``keytab-fix``."""
         from dcos_commons_amd.testing.cluster.marathon import REPO_ROOT
 
-        binary = os.path.join(REPO_ROOT, "native", "build", "sdk-bootstrap")
-        if os.path.exists(binary):
-            d = os.path.join(self.work_dir, "artifacts", "bootstrap")
-            os.makedirs(d, exist_ok=True)
-            shutil.copy2(binary, os.path.join(d, "bootstrap"))
-            self.artifacts["bootstrap.zip"] = d
+        for artifact, built, name in (("bootstrap.zip", "sdk-bootstrap", "bootstrap"),
+                                      ("keytab-fix.tar.gz", "keytab-fix", "keytab-fix")):
+            binary = os.path.join(REPO_ROOT, "native", "build", built)
+            if os.path.exists(binary):
+                d = os.path.join(self.work_dir, "artifacts", name)
+                os.makedirs(d, exist_ok=True)
+                shutil.copy2(binary, os.path.join(d, name))
+                self.artifacts[artifact] = d
 
     def register_artifact(self, basename: str, path: str) -> None:
         """Tasks fetching a URI that ends in ``basename`` get ``path`` (a file, or a directory
