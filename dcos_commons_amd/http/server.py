@@ -87,13 +87,15 @@ class ApiServer:
         self._stopping = threading.Event()
         self._serving = threading.Event()
         self._stopped = threading.Event()
+        # poll(2), as socketserver uses; built here, not on the serving thread inside a timed start
+        self._selector = selectors.PollSelector()
+        self._selector.register(self.httpd, selectors.EVENT_READ)
+        self._selector.register(self._wake_r, selectors.EVENT_READ)
 
     def serve(self) -> None:
         """Handles requests until ``stop()``; woken by a listening-socket event or the stop pipe."""
         self._serving.set()
-        sel = selectors.DefaultSelector()
-        sel.register(self.httpd, selectors.EVENT_READ)
-        sel.register(self._wake_r, selectors.EVENT_READ)
+        sel = self._selector
         try:
             while not self._stopping.is_set():
                 for key, _ in sel.select():

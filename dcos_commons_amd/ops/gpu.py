@@ -35,6 +35,7 @@ from __future__ import annotations
 import json
 import os
 import re
+import socket
 import subprocess
 from dataclasses import dataclass, field, replace
 from typing import Dict, Iterable, List, Mapping, Optional, Sequence, Tuple
@@ -70,6 +71,7 @@ class GpuDevice:
     vram_mib: int = 0
     hive: str = NO_HIVE             # xGMI hive id (hex), NO_HIVE without xGMI peers
     xgmi_peers: Tuple[int, ...] = ()  # HIP indices reachable over a direct xGMI link
+    xgmi_links: int = 0             # direct xGMI links to any GPU of the node, visible or not
     kfd_node: Optional[int] = None
     unique_id: str = ""
     device_id: int = 0
@@ -126,7 +128,8 @@ class GpuInventory:
     def to_dict(self) -> dict:
         return {"source": self.source, "devices": [
             {"index": d.index, "arch": d.arch, "model": d.model, "vendor": d.vendor, "compute_units": d.compute_units,
-             "vram_mib": d.vram_mib, "hive": d.hive, "xgmi_peers": list(d.xgmi_peers), "kfd_node": d.kfd_node,
+             "vram_mib": d.vram_mib, "hive": d.hive, "xgmi_peers": list(d.xgmi_peers), "xgmi_links": d.xgmi_links,
+             "kfd_node": d.kfd_node,
              "unique_id": d.unique_id, "device_id": d.device_id, "bdf": d.bdf} for d in self.devices]}
 
     @staticmethod
@@ -135,6 +138,7 @@ class GpuInventory:
                                        vendor=x.get("vendor", "amd"), compute_units=int(x.get("compute_units", 0)),
                                        vram_mib=int(x.get("vram_mib", 0)), hive=x.get("hive", NO_HIVE),
                                        xgmi_peers=tuple(int(p) for p in x.get("xgmi_peers", ())),
+                                       xgmi_links=int(x.get("xgmi_links", 0)),
                                        kfd_node=x.get("kfd_node"), unique_id=x.get("unique_id", ""),
                                        device_id=int(x.get("device_id", 0)), bdf=x.get("bdf", ""))
                              for x in d.get("devices", ())], d.get("source", "dict"))
@@ -184,9 +188,12 @@ def parse_kfd_topology(root: str) -> GpuInventory:
     except OSError:
         return GpuInventory([], "kfd")
     gpu_nodes: List[Tuple[int, Dict[str, int]]] = []
+    restricted = 0
     for n in names:
         text = _read(os.path.join(nodes_dir, n, "properties"))
-        if text is None:
+        if not text:
+            # a GPU this process was not granted: the kernel hands out an empty properties file
+            restricted += 1
             continue
         props = parse_kfd_properties(text)
         if props.get("simd_count", 0) > 0 and props.get("vendor_id", AMD_VENDOR_ID) in (AMD_VENDOR_ID, 0):
@@ -195,6 +202,7 @@ def parse_kfd_topology(root: str) -> GpuInventory:
     devices = []
     for i, (node, props) in enumerate(gpu_nodes):
         peers = set()
+        xgmi_to = set()
         for links in ("io_links", "p2p_links"):
             ldir = os.path.join(nodes_dir, str(node), links)
             try:
@@ -207,8 +215,10 @@ def parse_kfd_topology(root: str) -> GpuInventory:
                     continue
                 link = parse_kfd_properties(lp)
                 to = link.get("node_to")
-                if link.get("type") == IOLINK_TYPE_XGMI and to in index_of_node and to != node:
-                    peers.add(index_of_node[to])
+                if link.get("type") == IOLINK_TYPE_XGMI and to != node:
+                    xgmi_to.add(to)
+                    if to in index_of_node:
+                        peers.add(index_of_node[to])
         arch = arch_from_gfx_target_version(props.get("gfx_target_version", 0))
         simd_per_cu = props.get("simd_per_cu", 4) or 4
         hive_id = props.get("hive_id", 0)
@@ -216,11 +226,14 @@ def parse_kfd_topology(root: str) -> GpuInventory:
             index=i, arch=arch, model=_model_for(props.get("device_id", 0), arch),
             compute_units=props.get("simd_count", 0) // simd_per_cu,
             vram_mib=props.get("local_mem_size", 0) // (1 << 20),
-            hive=f"{hive_id:x}" if hive_id else NO_HIVE, xgmi_peers=tuple(sorted(peers)), kfd_node=node,
+            hive=f"{hive_id:x}" if hive_id else NO_HIVE, xgmi_peers=tuple(sorted(peers)), xgmi_links=len(xgmi_to),
+            kfd_node=node,
             unique_id=f"{props['unique_id']:x}" if props.get("unique_id") else "",
             device_id=props.get("device_id", 0),
             bdf=_bdf_from_location(props.get("domain", 0), props.get("location_id", 0))))
-    return GpuInventory(devices, "kfd")
+    inv = GpuInventory(devices, "kfd")
+    inv.restricted_nodes = restricted
+    return inv
 
 
 def _bdf_from_location(domain: int, location_id: int) -> str:
@@ -228,6 +241,85 @@ def _bdf_from_location(domain: int, location_id: int) -> str:
     if not location_id:
         return ""
     return f"{domain:04x}:{(location_id >> 8) & 0xFF:02x}:{(location_id >> 3) & 0x1F:02x}.{location_id & 0x7}"
+
+
+def parse_kfd_xgmi_links(root: str) -> Dict[int, set]:
+    """KFD node -> the nodes it has a direct xGMI io/p2p link to. Link files stay readable where a
+    node's own ``properties`` are not (a container granted one GPU of the node: the kernel's device
+    cgroup check empties the other GPUs' properties, and its own)."""
+    nodes_dir = os.path.join(root, "nodes")
+    out: Dict[int, set] = {}
+    try:
+        names = [n for n in os.listdir(nodes_dir) if n.isdigit()]
+    except OSError:
+        return out
+    for n in names:
+        for links in ("io_links", "p2p_links"):
+            ldir = os.path.join(nodes_dir, n, links)
+            try:
+                entries = os.listdir(ldir)
+            except OSError:
+                continue
+            for e in entries:
+                lp = _read(os.path.join(ldir, e, "properties"))
+                link = parse_kfd_properties(lp or "")
+                if link.get("type") == IOLINK_TYPE_XGMI and "node_to" in link and link["node_to"] != int(n):
+                    out.setdefault(int(n), set()).add(link["node_to"])
+                    out.setdefault(link["node_to"], set()).add(int(n))
+    return out
+
+
+def xgmi_hives(links: Mapping[int, Iterable[int]], label: str) -> Dict[int, str]:
+    """KFD node -> hive label: the connected components of the xGMI link graph. Without readable
+    ``hive_id``s the label is ``<label>:<lowest node of the component>`` (``label`` = the host: a
+    hive never spans hosts, so host plus component is unique across the cluster)."""
+    out: Dict[int, str] = {}
+    for start in sorted(links):
+        if start in out:
+            continue
+        comp, stack = set(), [start]
+        while stack:
+            x = stack.pop()
+            if x in comp:
+                continue
+            comp.add(x)
+            stack.extend(links.get(x, ()))
+        name = f"{label}:{min(comp)}"
+        for x in comp:
+            out[x] = name
+    return out
+
+
+def parse_amd_smi_list(text: str) -> Dict[int, int]:
+    """``amd-smi list --json``: visible GPU index -> its KFD topology node (``node_id``)."""
+    data = json.loads(text)
+    if isinstance(data, dict):
+        data = data.get("gpu_data", [data])
+    out = {}
+    for g in data or []:
+        if isinstance(g, dict) and "gpu" in g and isinstance(g.get("node_id"), int):
+            out[_int(g["gpu"])] = g["node_id"]
+    return out
+
+
+def attach_kfd_wiring(inv: GpuInventory, node_of: Mapping[int, int], links: Mapping[int, Iterable[int]],
+                      label: str) -> GpuInventory:
+    """Hive and xGMI peers of tool-enumerated devices from the KFD link graph, through the
+    device -> KFD node map of ``amd-smi list``."""
+    if not node_of or not links:
+        return inv
+    hive_of_node = xgmi_hives(links, label)
+    idx_of_node = {node_of[d.index]: d.index for d in inv.devices if d.index in node_of}
+    devices = []
+    for d in inv.devices:
+        node = node_of.get(d.index)
+        if node is None:
+            devices.append(d)
+            continue
+        peers = tuple(sorted(idx_of_node[p] for p in links.get(node, ()) if p in idx_of_node))
+        devices.append(replace(d, kfd_node=node, hive=hive_of_node.get(node, NO_HIVE), xgmi_peers=peers,
+                               xgmi_links=len(set(links.get(node, ())))))
+    return GpuInventory(devices, inv.source + "+kfd-links")
 
 
 # -- amd-smi ------------------------------------------------------------------------------------
@@ -248,6 +340,15 @@ def model_from_market_name(name: str) -> str:
     if m:
         return m.group(1).upper()
     return (name or "").replace("AMD Instinct", "").strip()
+
+
+def _best_model(market: str, device_id: int, arch: str) -> str:
+    """The marketing name's model, unless the PCI device id names the same part more precisely
+    (the MI355X box reports ``AMD Instinct MI355 OAM`` for device 0x75a3)."""
+    known = _DEVICE_MODELS.get(device_id, "")
+    if known and (not market or known.startswith(market)):
+        return known
+    return market or _model_for(device_id, arch)
 
 
 def parse_amd_smi_static(text: str) -> GpuInventory:
@@ -273,7 +374,8 @@ def parse_amd_smi_static(text: str) -> GpuInventory:
         arch = asic.get("target_graphics_version") or ""
         arch = arch if isinstance(arch, str) and arch.startswith("gfx") else ""
         devices.append(GpuDevice(
-            index=_int(g.get("gpu", i)), arch=arch, model=model_from_market_name(str(asic.get("market_name", ""))),
+            index=_int(g.get("gpu", i)), arch=arch,
+            model=_best_model(model_from_market_name(str(asic.get("market_name", ""))), _int(asic.get("device_id")), arch),
             compute_units=_int(asic.get("num_compute_units")), vram_mib=mib,
             device_id=_int(asic.get("device_id")), bdf=str(bus.get("bdf", "")) if bus.get("bdf") != "N/A" else ""))
     return GpuInventory(devices, "amd-smi")
@@ -293,11 +395,13 @@ def parse_rocminfo(text: str) -> GpuInventory:
             continue
         chip = re.search(r"\((0x[0-9a-fA-F]+)\)", fields.get("Chip ID", ""))
         node = fields.get("Node")
+        arch = fields.get("Name", "") if fields.get("Name", "").startswith("gfx") else ""
+        device_id = int(chip.group(1), 16) if chip else 0
+        # rocminfo's "Node" numbers the runtime's agents, not KFD topology nodes
         devices.append(GpuDevice(
-            index=len(devices), arch=fields.get("Name", "") if fields.get("Name", "").startswith("gfx") else "",
-            model=model_from_market_name(fields.get("Marketing Name", "")),
-            compute_units=_int(fields.get("Compute Unit", "0")), device_id=int(chip.group(1), 16) if chip else 0,
-            kfd_node=int(node) if node and node.isdigit() else None))
+            index=len(devices), arch=arch,
+            model=_best_model(model_from_market_name(fields.get("Marketing Name", "")), device_id, arch),
+            compute_units=_int(fields.get("Compute Unit", "0")), device_id=device_id))
     return GpuInventory(devices, "rocminfo")
 
 
@@ -334,7 +438,7 @@ def parse_visible_devices(value: Optional[str]) -> Optional[List[int]]:
     return out
 
 
-def apply_visibility(inv: GpuInventory, env: Mapping[str, str]) -> GpuInventory:
+def apply_visibility(inv: GpuInventory, env: Mapping[str, str], already_filtered: bool = False) -> GpuInventory:
     """Restrict and renumber as the ROCm runtime does: ``ROCR_VISIBLE_DEVICES`` selects among the
     node's devices, then ``HIP_VISIBLE_DEVICES`` among those; the survivors are numbered 0..n-1
     (xGMI peers are kept only among the survivors)."""
@@ -342,6 +446,10 @@ def apply_visibility(inv: GpuInventory, env: Mapping[str, str]) -> GpuInventory:
     for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES"):
         sel = parse_visible_devices(env.get(var))
         if sel is None:
+            continue
+        if already_filtered and any(i >= len(devices) for i in sel):
+            # the tools only saw the devices this container was granted: the selection named
+            # physical devices and has been applied already
             continue
         devices = [devices[i] for i in sel if 0 <= i < len(devices)]
         renumber = {d.index: n for n, d in enumerate(devices)}
@@ -380,12 +488,15 @@ def discover(env: Optional[Mapping[str, str]] = None, fixture_dir: Optional[str]
 def _discover(env: Mapping[str, str], fixture_dir: Optional[str], kfd_root: str, use_tools: bool) -> GpuInventory:
     base = parse_kfd_topology(kfd_root)
     refinements: List[GpuInventory] = []
-    smi_text = rocminfo_text = None
+    smi_text = list_text = rocminfo_text = None
     if fixture_dir:
         smi_text = _read(os.path.join(fixture_dir, "amd_smi_static.json"))
+        list_text = _read(os.path.join(fixture_dir, "amd_smi_list.json"))
         rocminfo_text = _read(os.path.join(fixture_dir, "rocminfo.txt"))
     elif use_tools:
         smi_text = _run(["amd-smi", "static", "--asic", "--bus", "--vram", "--json"])
+        if smi_text is not None and not base.devices:
+            list_text = _run(["amd-smi", "list", "--json"])
         if smi_text is None:
             rocminfo_text = _run(["rocminfo"])
     if smi_text:
@@ -395,11 +506,26 @@ def _discover(env: Mapping[str, str], fixture_dir: Optional[str], kfd_root: str,
             pass
     if rocminfo_text:
         refinements.append(parse_rocminfo(rocminfo_text))
-    if not base.devices:
-        # no KFD view (e.g. a container without /sys/class/kfd): the tools' own enumeration
-        base = next((r for r in refinements if r.devices), GpuInventory([], "none"))
-        refinements = [r for r in refinements if r is not base]
-    return apply_visibility(merge(base, *refinements), env)
+    if base.devices:
+        # with GPUs hidden from this container, the readable ones are already the granted subset
+        return apply_visibility(merge(base, *refinements), env,
+                                already_filtered=getattr(base, "restricted_nodes", 0) > 0)
+    # no readable KFD GPU nodes (no driver, or a container granted only some GPUs): the tools
+    # enumerate what this process may use; the KFD link graph (still readable) gives the wiring
+    base = next((r for r in refinements if r.devices), GpuInventory([], "none"))
+    refinements = [r for r in refinements if r is not base]
+    inv = merge(base, *refinements)
+    if list_text:
+        try:
+            node_of = parse_amd_smi_list(list_text)
+        except (ValueError, TypeError):
+            node_of = {}
+        if fixture_dir:
+            label = env.get("SDK_GPU_HOST_LABEL") or (_read(os.path.join(fixture_dir, "hostname")) or "").strip()
+        else:
+            label = env.get("SDK_GPU_HOST_LABEL") or socket.gethostname()
+        inv = attach_kfd_wiring(inv, node_of, parse_kfd_xgmi_links(kfd_root), label or "host")
+    return apply_visibility(inv, env, already_filtered=True)
 
 
 # -- device selection -----------------------------------------------------------------------------

@@ -134,8 +134,9 @@ def test_amd_smi_static_json():
 
 def test_rocminfo_gpu_agents():
     inv = G.parse_rocminfo(ROCMINFO)
+    # (rocminfo's "Node" numbers the runtime's agents, not KFD topology nodes: not kept)
     assert [(d.index, d.arch, d.model, d.kfd_node, d.compute_units) for d in inv.devices] == [
-        (0, "gfx950", "MI355X", 2, 256), (1, "gfx950", "MI355X", 3, 256)]
+        (0, "gfx950", "MI355X", None, 256), (1, "gfx950", "MI355X", None, 256)]
     assert inv.devices[0].device_id == 0x75A3
 
 
@@ -168,11 +169,41 @@ def test_visible_devices_restrict_and_renumber(tmp_path):
 
 @pytest.mark.skipif(not os.path.isdir(BOX_FIXTURE), reason="no recorded MI355X box dump")
 def test_recorded_mi355x_box_dump():
+    """The dump of the MI355X box (one GPU granted of its node's eight): only the granted GPU's KFD
+    properties are readable, its io_links show the node's seven xGMI links, amd-smi names the part
+    ``AMD Instinct MI355 OAM`` (device 0x75a3)."""
     inv = G.discover(env={}, fixture_dir=BOX_FIXTURE)
-    assert inv.count >= 1
-    assert {d.arch for d in inv.devices} == {"gfx950"}
-    assert all(d.model.startswith("MI35") for d in inv.devices)
-    assert all(d.compute_units == 256 for d in inv.devices)
+    assert inv.count == 1 and inv.source.startswith("kfd")
+    d = inv.devices[0]
+    assert (d.arch, d.model, d.compute_units, d.vram_mib) == ("gfx950", "MI355X", 256, 294896)
+    assert d.xgmi_links == 7 and d.xgmi_peers == () and d.hive not in ("", G.NO_HIVE)
+    assert d.bdf == "0000:f4:00.0" and d.kfd_node == 6
+    assert inv.attributes() == {"gpu_vendor": "amd", "gpu_model": "MI355X", "gpu_arch": "gfx950",
+                                "xgmi_hive": d.hive}
+    # the box's ROCR/HIP_VISIBLE_DEVICES=0 is already what the container was granted
+    assert G.discover(env={"ROCR_VISIBLE_DEVICES": "0", "HIP_VISIBLE_DEVICES": "0"}, fixture_dir=BOX_FIXTURE).count == 1
+    assert G.discover(env={"ROCR_VISIBLE_DEVICES": "5"}, fixture_dir=BOX_FIXTURE).count == 1
+    # rocminfo alone: the same part, no wiring
+    r = G.parse_rocminfo(open(os.path.join(BOX_FIXTURE, "rocminfo.txt")).read())
+    assert [(x.arch, x.model, x.compute_units) for x in r.devices] == [("gfx950", "MI355X", 256)]
+
+
+def test_restricted_kfd_tree_uses_amd_smi_list_and_link_graph(tmp_path):
+    """No readable GPU properties at all: amd-smi enumerates the granted GPUs, ``amd-smi list``
+    maps them to KFD nodes, and the still-readable xGMI links give hive and peers (the hive label
+    is host + lowest node of the link component: hives never span hosts)."""
+    node = _node(tmp_path, [0xA1] * 4 + [0xB2] * 4)
+    for n in range(2, 10):
+        open(os.path.join(node, "kfd", "nodes", str(n), "properties"), "w").close()
+    granted = json.loads(AMD_SMI_STATIC)[:2]
+    with open(os.path.join(node, "amd_smi_static.json"), "w") as f:
+        json.dump({"gpu_data": granted}, f)
+    with open(os.path.join(node, "amd_smi_list.json"), "w") as f:
+        json.dump([{"gpu": 0, "node_id": 3}, {"gpu": 1, "node_id": 7}], f)
+    inv = G.discover(env={"SDK_GPU_HOST_LABEL": "host-a"}, fixture_dir=node)
+    assert inv.count == 2 and "kfd-links" in inv.source
+    assert [(d.kfd_node, d.hive, d.xgmi_links) for d in inv.devices] == [(3, "host-a:2", 3), (7, "host-a:6", 3)]
+    assert all(d.xgmi_peers == () for d in inv.devices)     # granted GPUs sit in different hives
 
 
 # -- device selection --------------------------------------------------------------------------
