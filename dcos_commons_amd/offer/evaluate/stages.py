@@ -31,6 +31,8 @@ from dcos_commons_amd.offer.resources import (
     ResourceBuilder,
     get_disk_source,
     get_resource_id,
+    new_reservation,
+    new_root_volume,
 )
 from dcos_commons_amd.offer.taskdata import labels as L
 from dcos_commons_amd.specification.specs import (
@@ -85,15 +87,18 @@ def evaluate_simple_resource(stage, spec: ResourceSpec, resource_id: Optional[st
             spec.name, resource_id, spec), None)
     if resource_id is None:
         # a new reservation: consume_reservable_merged hands out exactly the spec's value
-        b = ResourceBuilder.from_spec(spec, None, namespace, framework_id)
         # an offered chunk that carried nothing beyond name/type/value builds to exactly what
-        # ResourceBuilder.from_spec(spec, new_id) produces, so it is built fresh and the task
-        # carries the same resource
+        # ResourceBuilder.from_spec(spec, new_id) produces, so it is built fresh (from the spec's
+        # wire template) and the task carries the same resource
         plain = not (mr.resource.HasField("disk") or mr.resource.HasField("provider_id")
                      or len(mr.resource.reservations) or mr.resource.HasField("reservation"))
-        resource = b.build() if plain else b.set_mesos_resource(mr).build()
+        if plain:
+            resource, new_id = new_reservation(spec, namespace, framework_id)
+        else:
+            b = ResourceBuilder.from_spec(spec, None, namespace, framework_id)
+            resource = b.set_mesos_resource(mr).build()
+            new_id = b.built_resource_id
         rec = ReserveOfferRecommendation(pool.offer, resource)
-        new_id = b.built_resource_id
         return ReserveEvaluationOutcome(EvaluationOutcome.pass_(
             stage, "Offer contains sufficient unreserved '%s', generated new resourceId: '%s' "
                    "for new reservation: '%s'", spec.name, new_id, spec,
@@ -394,9 +399,13 @@ class VolumeEvaluationStage(OfferEvaluationStage):
                 return res.outcome
             recs.extend(res.outcome.get_offer_recommendations())
             mr = res.outcome.mesos_resource
-            resource = ResourceBuilder.from_volume_spec(
-                self.spec, res.resource_id, self.namespace, self.persistence_id, None, None,
-                self.framework_id).set_mesos_resource(mr).build()
+            if res.resource is not None and self.persistence_id is None and len(res.resource_id or "") == 36:
+                # a new volume on a plain chunk: the reservation was built fresh, so is the volume
+                resource = new_root_volume(self.spec, res.resource_id, self.namespace, self.framework_id)
+            else:
+                resource = ResourceBuilder.from_volume_spec(
+                    self.spec, res.resource_id, self.namespace, self.persistence_id, None, None,
+                    self.framework_id).set_mesos_resource(mr).build()
         else:
             if self.resource_id is None:
                 mr = pool.consume_atomic(constants.DISK_RESOURCE_TYPE, self.spec)

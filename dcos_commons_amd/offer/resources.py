@@ -375,3 +375,64 @@ class ResourceBuilder:
                 r.disk.source.CopyFrom(self.disk_source)
         _set_value(r, self.value, fresh)
         return r
+
+
+# A placeholder resource_id of the length of every generated one (str(uuid4()): 36 characters),
+# swapped for the real id in the serialized template.
+_ID_PLACEHOLDER = "rrrrrrrr-rrrr-4rrr-8rrr-rrrrrrrrrrrr"
+_NEW_RESERVATIONS: dict = {}
+
+
+def new_reservation(spec: ResourceSpec, namespace: Optional[str], framework_id: Optional[str]):
+    """``ResourceBuilder.from_spec(spec, None, namespace, framework_id).build()`` for a new
+    reservation of a plain offered chunk, and its generated resource id, from a per-spec wire
+    template: every pod of a pod type reserves the same cpus/mem/disk/gpus with the same role,
+    principal and labels, so only the resource id differs. The template is built once with a
+    placeholder id of the same length, which is replaced in the serialized bytes; the result is
+    parsed in C instead of assembled field by field in Python (about 8 resources per pod launch)."""
+    pre = capabilities.get_instance().supports_pre_reserved_resources
+    key = (id(spec), namespace, framework_id, pre)
+    hit = _NEW_RESERVATIONS.get(key)
+    if hit is None or hit[0] is not spec:
+        b = ResourceBuilder.from_spec(spec, _ID_PLACEHOLDER, namespace, framework_id)
+        data = b.build().SerializeToString()
+        if data.count(_ID_PLACEHOLDER.encode()) != 1:
+            hit = (spec, None)
+        else:
+            hit = (spec, data)
+        if len(_NEW_RESERVATIONS) > 4096:
+            _NEW_RESERVATIONS.clear()
+        _NEW_RESERVATIONS[key] = hit
+    rid = uuid4_str()
+    if hit[1] is None:   # a layout the template cannot stand for: build it the long way
+        b = ResourceBuilder.from_spec(spec, rid, namespace, framework_id)
+        return b.build(), rid
+    return P.Resource.FromString(hit[1].replace(_ID_PLACEHOLDER.encode(), rid.encode(), 1)), rid
+
+
+_PERSISTENCE_PLACEHOLDER = "pppppppp-pppp-4ppp-8ppp-pppppppppppp"
+_NEW_ROOT_VOLUMES: dict = {}
+
+
+def new_root_volume(spec: VolumeSpec, resource_id: str, namespace: Optional[str],
+                    framework_id: Optional[str]) -> P.Resource:
+    """``ResourceBuilder.from_volume_spec(spec, resource_id, namespace, None, None, None,
+    framework_id).build()`` of a new ROOT volume on a plain disk chunk (a fresh persistence id),
+    from a per-spec wire template with placeholder resource and persistence ids (see
+    ``new_reservation``)."""
+    pre = capabilities.get_instance().supports_pre_reserved_resources
+    key = (id(spec), namespace, framework_id, pre)
+    hit = _NEW_ROOT_VOLUMES.get(key)
+    if hit is None or hit[0] is not spec:
+        b = ResourceBuilder.from_volume_spec(spec, _ID_PLACEHOLDER, namespace, _PERSISTENCE_PLACEHOLDER, None, None,
+                                             framework_id)
+        data = b.build().SerializeToString()
+        ok = data.count(_ID_PLACEHOLDER.encode()) == 1 and data.count(_PERSISTENCE_PLACEHOLDER.encode()) == 1
+        hit = (spec, data if ok else None)
+        if len(_NEW_ROOT_VOLUMES) > 4096:
+            _NEW_ROOT_VOLUMES.clear()
+        _NEW_ROOT_VOLUMES[key] = hit
+    if hit[1] is None:
+        return ResourceBuilder.from_volume_spec(spec, resource_id, namespace, None, None, None, framework_id).build()
+    data = hit[1].replace(_ID_PLACEHOLDER.encode(), resource_id.encode(), 1)
+    return P.Resource.FromString(data.replace(_PERSISTENCE_PLACEHOLDER.encode(), uuid4_str().encode(), 1))

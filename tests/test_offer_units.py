@@ -425,3 +425,25 @@ def test_unreserve_mount_disk_keeps_only_the_source(refined):
     expected.disk.Clear()
     expected.disk.source.CopyFrom(r.disk.source)
     assert got == expected
+
+
+@pytest.mark.parametrize("pre_reserved", [ANY_ROLE, "slave_public"])
+@pytest.mark.parametrize("namespace", [None, "ns"])
+def test_wire_template_reservations_equal_the_builder(refined, pre_reserved, namespace):
+    """``new_reservation`` / ``new_root_volume`` (the per-spec wire templates the evaluator uses for
+    new reservations on plain chunks) build exactly what ResourceBuilder builds for the same ids."""
+    from dcos_commons_amd.offer.resources import get_persistence_id, get_resource_id, new_reservation, new_root_volume
+
+    spec = ResourceSpec(name="cpus", value=CPU_VALUE, role=U.ROLE,
+                        principal=U.PRINCIPAL, pre_reserved_role=pre_reserved)
+    for _ in range(2):   # template built, then reused
+        r, rid = new_reservation(spec, namespace, "fw-id")
+        assert get_resource_id(r) == rid
+        assert r == ResourceBuilder.from_spec(spec, rid, namespace, "fw-id").build()
+    vol = VolumeSpec.create_root_volume(64, U.CONTAINER_PATH, U.ROLE, pre_reserved, U.PRINCIPAL)
+    for _ in range(2):
+        r, rid = new_reservation(vol, namespace, "fw-id")
+        v = new_root_volume(vol, rid, namespace, "fw-id")
+        pid = get_persistence_id(v)
+        assert get_resource_id(v) == rid and pid and pid != rid
+        assert v == ResourceBuilder.from_volume_spec(vol, rid, namespace, pid, None, None, "fw-id").build()
