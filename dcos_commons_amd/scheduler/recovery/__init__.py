@@ -144,6 +144,7 @@ class DefaultRecoveryPlanManager(PlanManager):
         self.namespace = namespace
         self.overriders = list(overriders or [])
         self._plan = DefaultPlan(constants.RECOVERY_PLAN_NAME, [], ParallelStrategy())
+        self._scan_memo: Dict[str, tuple] = {}   # task name -> (info bytes, status bytes, info, status, flags)
         self._lock = threading.RLock()
         self.logger = get_logger(__name__, namespace)
 
@@ -234,15 +235,52 @@ class DefaultRecoveryPlanManager(PlanManager):
                 out.append(req)
         return out
 
+    def _scan(self):
+        """Every task's TaskInfo and TaskStatus, plus which tasks need recovery and which were marked
+        gone by the operator. The recovery plan is regenerated on every candidate query (each offer
+        cycle and status pass, DefaultRecoveryPlanManager.java:164), which made every query parse and
+        classify every task of the service; the classification depends only on the task's stored
+        TaskInfo and TaskStatus (and the immutable config they point at), so it is kept per task and
+        redone only for tasks whose stored bytes changed."""
+        infos_b = self.state_store.fetch_tasks_bytes()
+        statuses_b = self.state_store.fetch_statuses_bytes(list(infos_b))
+        memo, fresh = self._scan_memo, {}
+        infos, statuses, needing, gone = [], [], [], []
+        for name, ib in infos_b.items():
+            sb = statuses_b.get(name)
+            hit = memo.get(name)
+            if hit is None or hit[0] is not ib or hit[1] is not sb:
+                if hit is not None and hit[0] == ib and hit[1] == sb:
+                    hit = (ib, sb) + hit[2:]
+                else:
+                    info = P.TaskInfo.FromString(ib)
+                    status = P.TaskStatus.FromString(sb) if sb is not None else None
+                    need = (status is not None and
+                            bool(task_utils.get_tasks_needing_recovery(self.config_store, [info], [status])))
+                    is_gone = (status is not None and status.state == P.TASK_GONE_BY_OPERATOR
+                               and status.task_id.value == info.task_id.value
+                               and not task_utils.is_permanently_failed(info))
+                    hit = (ib, sb, info, status, need, is_gone)
+            fresh[name] = hit
+            infos.append(hit[2])
+            if hit[3] is not None:
+                statuses.append(hit[3])
+            if hit[4]:
+                needing.append(hit[2])
+            if hit[5]:
+                gone.append(hit[2])
+        self._scan_memo = fresh
+        return infos, statuses, needing, gone
+
     def _new_failed_pods(self, dirty_assets) -> List[PodInstanceRequirement]:
-        infos = self.state_store.fetch_tasks()
-        statuses = self.state_store.fetch_statuses()
-        replace = task_utils.get_tasks_for_replacement(statuses, infos)
+        infos, statuses, needing, replace = self._scan()
         if replace:
             set_permanently_failed(self.state_store, replace)
-            infos = self.state_store.fetch_tasks()
-        failed_tasks = [t for t in task_utils.get_tasks_needing_recovery(self.config_store, infos, statuses)
-                        if t.name in self.recoverable_task_names]
+            infos, statuses, needing, _ = self._scan()
+        failed_tasks = [t for t in needing if t.name in self.recoverable_task_names]
+        if not failed_tasks and not any(not s.is_complete() for ph in self._plan.get_children()
+                                        for s in ph.get_children()):
+            return []
         failed_pods = task_utils.get_pod_requirements(self.config_store, infos, statuses, failed_tasks,
                                                       backoff_mod.get_instance())
         failed_pods = [p for p in failed_pods if not asset_conflicts(p, dirty_assets)]

@@ -257,6 +257,17 @@ class StateStore:
             raise StateStoreException(Reason.SERIALIZATION_ERROR, str(e)) from e
         return t
 
+    def fetch_statuses_bytes(self, names: Optional[List[str]] = None) -> Dict[str, bytes]:
+        """Serialized TaskStatus by task name, read in one persister call (tasks without one are
+        left out), for callers that memoize on the exact bytes."""
+        names = self.fetch_task_names() if names is None else names
+        paths = {self._task_status_path(n): n for n in names}
+        try:
+            raw = self.persister.get_many(list(paths))
+        except PersisterException as e:
+            raise StateStoreException(e.reason, str(e)) from e
+        return {n: raw[p] for p, n in paths.items() if raw.get(p) is not None}
+
     def fetch_statuses(self) -> List[P.TaskStatus]:
         """Every stored TaskStatus, read in one persister call (tasks without one are skipped)."""
         paths = [self._task_status_path(n) for n in self.fetch_task_names()]

@@ -35,6 +35,10 @@ class _NullLock:
 _NULL = _NullLock()
 
 
+_SPLIT: Dict[str, List[str]] = {}   # path -> its elements (never mutated by callers)
+_SPLIT_MAX = 65536
+
+
 class MemPersister(Persister):
     def __init__(self, locking: bool = True, data: Optional[Mapping[str, bytes]] = None):
         self._root = _Node()
@@ -48,7 +52,17 @@ class MemPersister(Persister):
 
     # -- internals -----------------------------------------------------------------------
     def _node(self, path, create: bool) -> Optional[_Node]:
-        elems = path if isinstance(path, list) else get_path_elements(path)
+        if isinstance(path, list):
+            elems = path
+        else:
+            # the state store asks for the same few hundred paths over and over (every task's
+            # TaskInfo/TaskStatus on each plan query): split each path string once
+            elems = _SPLIT.get(path)
+            if elems is None:
+                elems = get_path_elements(path)
+                if len(_SPLIT) >= _SPLIT_MAX:
+                    _SPLIT.clear()
+                _SPLIT[path] = elems
         cur = self._root
         for e in elems:
             nxt = cur.children.get(e)
