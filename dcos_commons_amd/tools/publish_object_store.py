@@ -1,11 +1,11 @@
-"""Publish a built package to an object store: artifacts plus a stub universe whose artifact URLs
-point at the store (reference: tools/publish_aws.py, tools/publish_azure.py).
+"""The provider-independent half of publishing a built package to an object store: render the
+stub universe against the store's HTTP directory, upload it first and the artifacts next to it,
+and report the universe URL (reference: the shared flow of tools/publish_aws.py and
+tools/publish_azure.py). The providers (``publish_aws``, ``publish_azure``) pick the destination.
 
-``S3_BUCKET`` / ``S3_DIR_PATH`` (AWS) or ``AZURE_STORAGE_ACCOUNT`` / ``AZURE_CONTAINER`` /
-``AZURE_DIR_PATH`` (Azure) choose the destination; a random ``autodelete7d/<pkg>-<ts>-<rand>``
-directory keeps concurrent publishes apart as in the reference. ``UNIVERSE_URL_PREFIX`` is
-prepended to the stub universe URL (the reference's universe-converter), ``UNIVERSE_URL_PATH``
-receives the URL, and ``WORKSPACE`` gets the ``<version>.properties`` file for CI.
+``UNIVERSE_URL_PREFIX`` is prepended to the stub universe URL (the reference's
+universe-converter), ``UNIVERSE_URL_PATH`` receives the URL, and ``WORKSPACE`` gets the
+``<version>.properties`` file for CI.
 """
 from __future__ import annotations
 
@@ -24,22 +24,10 @@ LOGGER = logging.getLogger(__name__)
 UNIVERSE_CONTENT_TYPE = "application/vnd.dcos.universe.repo+json;charset=utf-8"
 
 
-def _unique_dir(package_name: str) -> str:
-    rand = "".join(random.choice(string.ascii_lowercase + string.digits) for _ in range(8))
-    return f"autodelete7d/{package_name}-{time.strftime('%Y%m%d-%H%M%S')}-{rand}"
-
-
-def s3_directory_from_env(package_name: str) -> str:
-    bucket = os.environ.get("S3_BUCKET", "infinity-artifacts")
-    path = os.environ.get("S3_DIR_PATH") or _unique_dir(package_name)
-    return f"s3://{bucket}/{path.strip('/')}"
-
-
-def azure_directory_from_env(package_name: str) -> str:
-    account = os.environ.get("AZURE_STORAGE_ACCOUNT", "infinityartifacts")
-    container = os.environ.get("AZURE_CONTAINER", "artifacts")
-    path = os.environ.get("AZURE_DIR_PATH") or _unique_dir(package_name)
-    return f"https://{account}.blob.core.windows.net/{container}/{path.strip('/')}"
+def unique_dir_name() -> str:
+    """``<yyyymmdd-HHMMSS>-<16 random letters/digits>``: concurrent publishes never collide."""
+    rand = "".join(random.SystemRandom().choice(string.ascii_letters + string.digits) for _ in range(16))
+    return f"{time.strftime('%Y%m%d-%H%M%S')}-{rand}"
 
 
 class ObjectStorePublisher:
@@ -83,19 +71,9 @@ class ObjectStorePublisher:
                 f.write(url + "\n")
 
 
-def aws_publisher(package_name, package_version, input_dir_path, artifact_paths) -> ObjectStorePublisher:
-    dry = bool(os.environ.get("DRY_RUN"))
-    return ObjectStorePublisher(package_name, package_version, input_dir_path, artifact_paths,
-                                S3Uploader(s3_directory_from_env(package_name), dry), dry)
-
-
-def azure_publisher(package_name, package_version, input_dir_path, artifact_paths) -> ObjectStorePublisher:
-    dry = bool(os.environ.get("DRY_RUN"))
-    return ObjectStorePublisher(package_name, package_version, input_dir_path, artifact_paths,
-                                AzureUploader(azure_directory_from_env(package_name), dry), dry)
-
-
-def main(argv: Sequence[str], make=aws_publisher) -> int:
+def main(argv: Sequence[str], make) -> int:
+    """Shared command line of ``publish_aws`` / ``publish_azure``: ``make`` builds the provider's
+    publisher for (package name, version, template dir, artifacts)."""
     if len(argv) < 3:
         print("Syntax: {} <package-name> <template-package-dir> [artifact files ...]".format(argv[0]),
               file=sys.stderr)
@@ -106,5 +84,3 @@ def main(argv: Sequence[str], make=aws_publisher) -> int:
     return 0
 
 
-if __name__ == "__main__":
-    sys.exit(main(sys.argv))

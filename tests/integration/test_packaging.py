@@ -76,11 +76,14 @@ def test_uninstall_packaged_service(built):
 def test_install_from_object_store(built, store, tmp_path, monkeypatch):
     """tools/publish_aws.py / publish_azure.py: artifacts and the stub universe go to a bucket
     (container) under a unique directory; the repo URL is the bucket's HTTP address."""
-    from dcos_commons_amd.tools.publish_object_store import aws_publisher, azure_publisher
+    from dcos_commons_amd.tools.publish_aws import aws_publisher
+    from dcos_commons_amd.tools.publish_azure import azure_publisher
     from dcos_commons_amd.tools.universe.uploaders import LocalObjectStore
 
     c, _, artifacts, _ = built
     monkeypatch.setenv("SDK_OBJECT_STORE_ROOT", str(tmp_path / "store"))
+    monkeypatch.setenv("AZURE_STORAGE_ACCOUNT", "infinityartifacts")
+    monkeypatch.setenv("AZURE_CONTAINER_NAME", "artifacts")
     monkeypatch.setenv("UNIVERSE_URL_PATH", str(tmp_path / "url.txt"))
     version = f"3.0.0-{store}"
     make = aws_publisher if store == "aws" else azure_publisher

@@ -307,3 +307,40 @@ def test_validate_pip_freeze():
     import yaml
 
     assert v.validate(f"PyYAML=={yaml.__version__}\n") == []
+
+
+def test_publish_aws_destination_from_env(monkeypatch):
+    """tools/publish_aws.py ``s3_urls_from_env``: bucket / dir path / dir name defaults and the
+    ``S3_URL`` / ``ARTIFACT_DIR`` overrides."""
+    from dcos_commons_amd.tools import publish_aws as A
+
+    for k in ("S3_BUCKET", "S3_DIR_PATH", "S3_DIR_NAME", "S3_URL", "ARTIFACT_DIR"):
+        monkeypatch.delenv(k, raising=False)
+    s3, http = A.s3_urls_from_env("hello-world")
+    assert s3.startswith("s3://infinity-artifacts/autodelete7d/hello-world/") and http == ""
+    name = s3.rsplit("/", 1)[1]
+    assert len(name.split("-")) == 3 and len(name.split("-")[2]) == 16   # <date>-<time>-<16 random>
+    monkeypatch.setenv("S3_BUCKET", "b")
+    monkeypatch.setenv("S3_DIR_PATH", "/nightly/")
+    monkeypatch.setenv("S3_DIR_NAME", "run-7")
+    assert A.s3_urls_from_env("pkg") == ("s3://b/nightly/pkg/run-7", "")
+    monkeypatch.setenv("S3_URL", "s3://other/x/y/")
+    monkeypatch.setenv("ARTIFACT_DIR", "https://cdn.example.com/x/y/")
+    assert A.s3_urls_from_env("pkg") == ("s3://other/x/y", "https://cdn.example.com/x/y")
+    monkeypatch.setenv("S3_URL", "https://not-s3")
+    with pytest.raises(ValueError):
+        A.s3_urls_from_env("pkg")
+
+
+def test_publish_azure_requires_account_and_container(monkeypatch, tmp_path):
+    from dcos_commons_amd.tools import publish_azure as Z
+
+    monkeypatch.delenv("AZURE_STORAGE_ACCOUNT", raising=False)
+    monkeypatch.setenv("AZURE_CONTAINER_NAME", "c")
+    with pytest.raises(ValueError, match="AZURE_STORAGE_ACCOUNT"):
+        Z.azure_publisher("pkg", "1.0", str(tmp_path), [])
+    monkeypatch.setenv("AZURE_STORAGE_ACCOUNT", "acct")
+    monkeypatch.delenv("AZURE_DIR_PATH", raising=False)
+    assert Z.azure_directory_from_env() == "https://acct.blob.core.windows.net/c"
+    monkeypatch.setenv("AZURE_DIR_PATH", "/nested/dir/")
+    assert Z.azure_directory_from_env() == "https://acct.blob.core.windows.net/c/nested/dir"
