@@ -18,7 +18,6 @@ import time
 from typing import List, Sequence
 
 from dcos_commons_amd.tools.universe import Package, PackageManager, UniversePackageBuilder, Version
-from dcos_commons_amd.tools.universe.uploaders import AzureUploader, S3Uploader
 
 LOGGER = logging.getLogger(__name__)
 UNIVERSE_CONTENT_TYPE = "application/vnd.dcos.universe.repo+json;charset=utf-8"
