@@ -26,12 +26,14 @@ new task RUNNING and ready with ``/v1/plans/recovery`` at 200; replace MTTR: fro
 from __future__ import annotations
 
 import argparse
+import http.client
 import json
 import logging
 import statistics
 import threading
 import time
 import urllib.error
+import urllib.parse
 import urllib.request
 from typing import Callable, Dict, List, Optional
 
@@ -137,11 +139,25 @@ class ClusterBench:
         return best
 
     def _wait_plan(self, base: str, plan: str) -> float:
+        """Polls ``GET /v1/plans/<plan>`` until it answers 200, over one keep-alive connection (a
+        new connection per poll would cost the scheduler a connection thread every millisecond,
+        taken from the status processing being measured)."""
         deadline = time.monotonic() + self.timeout_s
-        while time.monotonic() < deadline:
-            if _get(f"{base}/v1/plans/{plan}") == 200:
-                return time.perf_counter()
-            time.sleep(POLL_S)
+        u = urllib.parse.urlsplit(base)
+        conn = http.client.HTTPConnection(u.hostname, u.port, timeout=5)
+        try:
+            while time.monotonic() < deadline:
+                try:
+                    conn.request("GET", f"/v1/plans/{plan}")
+                    r = conn.getresponse()
+                    r.read()
+                    if r.status == 200:
+                        return time.perf_counter()
+                except (OSError, http.client.HTTPException):
+                    conn.close()
+                time.sleep(POLL_S)
+        finally:
+            conn.close()
         raise TimeoutError(f"/v1/plans/{plan} never answered 200")
 
     def _wait_idle(self, svc: str) -> None:

@@ -10,6 +10,7 @@ from __future__ import annotations
 
 import logging
 import threading
+from typing import List
 
 from dcos_commons_amd import metrics, trace
 from dcos_commons_amd.mesos import protos as P
@@ -154,44 +155,67 @@ class FrameworkScheduler:
 
     def status_update(self, driver, status: P.TaskStatus) -> None:
         try:
-            LOGGER.info("Received status update for taskId=%s state=%s message='%s'", status.task_id.value,
-                        P.TaskState.Name(status.state), status.message)
-            metrics.record_status(status)
-            # a status during explicit reconciliation may end it: wake the loop whatever the state
-            awaiting = getattr(self.client, "awaiting_reconciliation", None)
-            reconciling = awaiting is not None and awaiting()
+            reconciling = self._received(status)
             with trace.span("status", "status", task=status.task_id.value, state=P.TaskState.Name(status.state)):
                 resp = self.client.task_status(status)
-            relaunch_kill = task_killer.ends_relaunch_kill(status)
-            eligible = task_killer.update(status)
-            if resp.result == TaskStatusResult.UNKNOWN_TASK:
-                if eligible:
-                    LOGGER.info("Received status update for unknown task, marking task to be killed: %s",
-                                status.task_id.value)
-                    task_killer.kill_task(status.task_id)
-                else:
-                    LOGGER.warning("Received status update for unknown task, but task should not be killed "
-                                   "again: %s", status.task_id.value)
-            # A task that ended (finished, failed, killed: after a kill issued for a relaunch
-            # too) released reservations the plans reuse: an in-place relaunch or recovery, or
-            # the pod's next step. A revive has the master offer them now, and that offer wakes
-            # the loop for the relaunch (after a relaunch kill no full cycle runs first: the
-            # offers in hand cannot hold them). For a replacement placed elsewhere the offer
-            # carries the stale reservations to release, which a scheduler that has gone idle
-            # (suppressed) would otherwise never be offered.
-            released = status.state in _RELEASING_STATES and resp.result != TaskStatusResult.UNKNOWN_TASK
-            work = can_create_work(status) and not relaunch_kill
-            if work and status.state == P.TASK_RUNNING:
-                # a readiness result: does any plan have a step it could unblock, or is this the
-                # end of the last launched step (the cycle then suppresses offers)?
-                useful = getattr(self.client, "offer_cycle_useful", None)
-                work = useful is None or useful()
-            if resp.result == TaskStatusResult.UNKNOWN_TASK or reconciling or work:
-                self.offer_processor.kick()
-            if relaunch_kill or released:
-                self.offer_processor.reoffer_released()
+            self._processed(status, resp, reconciling)
         except Exception as e:  # noqa: BLE001
             self._exit(e)
+
+    def status_updates(self, driver, statuses: List[P.TaskStatus]) -> None:
+        """Status updates that arrived together on the event stream (the driver calls this
+        instead of ``status_update`` when it has read several at once, and acknowledges them
+        after it returns): the client stores them in one transaction."""
+        if len(statuses) == 1:
+            self.status_update(driver, statuses[0])
+            return
+        try:
+            flags = [self._received(s) for s in statuses]
+            batch = getattr(self.client, "task_statuses", None)   # clients not built on MesosEventClient
+            with trace.span("status_batch", "status", n=len(statuses)):
+                resps = batch(statuses) if batch is not None else [self.client.task_status(s) for s in statuses]
+            for status, resp, reconciling in zip(statuses, resps, flags):
+                self._processed(status, resp, reconciling)
+        except Exception as e:  # noqa: BLE001
+            self._exit(e)
+
+    def _received(self, status: P.TaskStatus) -> bool:
+        LOGGER.info("Received status update for taskId=%s state=%s message='%s'", status.task_id.value,
+                    P.TaskState.Name(status.state), status.message)
+        metrics.record_status(status)
+        # a status during explicit reconciliation may end it: wake the loop whatever the state
+        awaiting = getattr(self.client, "awaiting_reconciliation", None)
+        return awaiting is not None and awaiting()
+
+    def _processed(self, status: P.TaskStatus, resp, reconciling: bool) -> None:
+        relaunch_kill = task_killer.ends_relaunch_kill(status)
+        eligible = task_killer.update(status)
+        if resp.result == TaskStatusResult.UNKNOWN_TASK:
+            if eligible:
+                LOGGER.info("Received status update for unknown task, marking task to be killed: %s",
+                            status.task_id.value)
+                task_killer.kill_task(status.task_id)
+            else:
+                LOGGER.warning("Received status update for unknown task, but task should not be killed "
+                               "again: %s", status.task_id.value)
+        # A task that ended (finished, failed, killed: after a kill issued for a relaunch
+        # too) released reservations the plans reuse: an in-place relaunch or recovery, or
+        # the pod's next step. A revive has the master offer them now, and that offer wakes
+        # the loop for the relaunch (after a relaunch kill no full cycle runs first: the
+        # offers in hand cannot hold them). For a replacement placed elsewhere the offer
+        # carries the stale reservations to release, which a scheduler that has gone idle
+        # (suppressed) would otherwise never be offered.
+        released = status.state in _RELEASING_STATES and resp.result != TaskStatusResult.UNKNOWN_TASK
+        work = can_create_work(status) and not relaunch_kill
+        if work and status.state == P.TASK_RUNNING:
+            # a readiness result: does any plan have a step it could unblock, or is this the
+            # end of the last launched step (the cycle then suppresses offers)?
+            useful = getattr(self.client, "offer_cycle_useful", None)
+            work = useful is None or useful()
+        if resp.result == TaskStatusResult.UNKNOWN_TASK or reconciling or work:
+            self.offer_processor.kick()
+        if relaunch_kill or released:
+            self.offer_processor.reoffer_released()
 
     def offer_rescinded(self, driver, offer_id: P.OfferID) -> None:
         try:

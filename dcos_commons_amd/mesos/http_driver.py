@@ -11,6 +11,9 @@ in ``framework/SchedulerDriverFactory.java:80-158`` and uses the V1 API by defau
   reconcilers) so each thread keeps its own keep-alive connection;
 * implicit acknowledgements: after ``status_update`` returns, updates that carry a ``uuid`` are
   ACKNOWLEDGEd (the adapter's default);
+* UPDATE events read from the stream together (the scheduler fell behind while a previous one was
+  stored) go to ``scheduler.status_updates`` in one call when the scheduler has it, so they are
+  persisted in one transaction; each is still acknowledged only after that call returns;
 * ``307 Temporary Redirect`` follows the leading master; ``503`` (no leader yet) backs off;
 * heartbeats: the stream is considered dead after ``heartbeat_misses`` intervals of silence.
 
@@ -403,15 +406,56 @@ class V1HttpSchedulerDriver(SchedulerDriver):
 
     def _consume(self, resp) -> None:
         dec = recordio.Decoder()
+        # a chunked stream is de-chunked here from the socket's buffered reader: every event that
+        # has arrived is decoded in one pass (http.client returns one chunk per read)
+        chunks = recordio.ChunkedDecoder() if resp.chunked else None
+        read = resp.fp.read1 if chunks is not None else resp.read1
         while not self._stopped.is_set():
             try:
-                data = resp.read1(65536)
+                data = read(65536)
             except socket.timeout:
                 raise OSError("missed heartbeats") from None
             if not data:
                 return
+            if chunks is not None:
+                data = chunks.feed(data)
+            updates: List[P.TaskStatus] = []
             for rec in dec.feed(data):
-                self._on_event(decode_message(P.Event, rec, self.content_type))
+                ev = decode_message(P.Event, rec, self.content_type)
+                if ev.type == P.Event.UPDATE:
+                    # updates read together are handed over together (order kept): a scheduler
+                    # that fell behind stores them in one transaction instead of one each
+                    updates.append(ev.update.status)
+                    continue
+                if updates:
+                    self._on_updates(updates)
+                    updates = []
+                self._on_event(ev)
+            if updates:
+                self._on_updates(updates)
+            if chunks is not None and chunks.done:
+                return
+
+    def _on_updates(self, statuses: List[P.TaskStatus]) -> None:
+        if len(statuses) == 1 or getattr(self.scheduler, "status_updates", None) is None:
+            for status in statuses:
+                self._on_update(status)
+            return
+        self._call_scheduler("status_updates", statuses)
+        if self.implicit_acknowledgements:
+            for status in statuses:
+                self._acknowledge(status)
+
+    def _on_update(self, status: P.TaskStatus) -> None:
+        self._call_scheduler("status_update", status)
+        if self.implicit_acknowledgements:
+            self._acknowledge(status)
+
+    def _acknowledge(self, status: P.TaskStatus) -> None:
+        try:
+            self.acknowledge_status_update(status)
+        except MesosCallError as e:
+            LOGGER.warning("ACKNOWLEDGE of %s failed: %s", status.task_id.value, e)
 
     def _call_scheduler(self, name: str, *args) -> None:
         fn = getattr(self.scheduler, name, None)
@@ -443,13 +487,7 @@ class V1HttpSchedulerDriver(SchedulerDriver):
         elif t == P.Event.RESCIND:
             self._call_scheduler("offer_rescinded", ev.rescind.offer_id)
         elif t == P.Event.UPDATE:
-            status = ev.update.status
-            self._call_scheduler("status_update", status)
-            if self.implicit_acknowledgements:
-                try:
-                    self.acknowledge_status_update(status)
-                except MesosCallError as e:
-                    LOGGER.warning("ACKNOWLEDGE of %s failed: %s", status.task_id.value, e)
+            self._on_update(ev.update.status)
         elif t == P.Event.MESSAGE:
             m = ev.message
             self._call_scheduler("framework_message", m.executor_id, m.agent_id, m.data)

@@ -67,3 +67,57 @@ def iter_records(read: Callable[[int], bytes], chunk: int = 65536) -> Iterator[b
                 raise RecordIOError("stream ended inside a record")
             return
         yield from dec.feed(data)
+
+
+class ChunkedDecoder:
+    """Incremental HTTP/1.1 ``Transfer-Encoding: chunked`` decoder (``<hex size>[;ext]\\r\\n<data>\\r\\n``
+    ... ``0\\r\\n<trailers>\\r\\n``). ``http.client`` hands a chunked body over one chunk per
+    ``read1``; reading the socket directly and de-chunking here returns everything that has
+    arrived, so a reader that fell behind gets every queued event in one pass. ``done`` turns true
+    after the last (zero-size) chunk; bytes after it are ignored."""
+
+    _MAX_LINE = 4096
+
+    def __init__(self):
+        self._buf = bytearray()
+        self._left = 0            # data bytes still to come in the current chunk
+        self._crlf = False        # the CRLF that ends a chunk's data is still to come
+        self.done = False
+
+    def feed(self, data: bytes) -> bytes:
+        self._buf += data
+        out = bytearray()
+        while not self.done:
+            if self._left:
+                take = min(self._left, len(self._buf))
+                if not take:
+                    break
+                out += self._buf[:take]
+                del self._buf[:take]
+                self._left -= take
+                if self._left:
+                    break
+                self._crlf = True
+            if self._crlf:
+                if len(self._buf) < 2:
+                    break
+                if self._buf[:2] != b"\r\n":
+                    raise RecordIOError("chunk data not followed by CRLF")
+                del self._buf[:2]
+                self._crlf = False
+            nl = self._buf.find(b"\r\n")
+            if nl < 0:
+                if len(self._buf) > self._MAX_LINE:
+                    raise RecordIOError("chunk size line too long")
+                break
+            line = bytes(self._buf[:nl]).split(b";", 1)[0].strip()
+            try:
+                size = int(line, 16)
+            except ValueError:
+                raise RecordIOError(f"bad chunk size {line[:32]!r}") from None
+            del self._buf[:nl + 2]
+            if size == 0:
+                self.done = True
+                break
+            self._left = size
+        return bytes(out)

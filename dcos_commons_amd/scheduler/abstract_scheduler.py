@@ -130,6 +130,66 @@ class AbstractScheduler(MesosEventClient):
 
     def task_status(self, status) -> TaskStatusResponse:
         self.launch_watchdog.update(status)
+        return self.task_status_processed(self._unknown_as_lost(status))
+
+    def task_statuses(self, statuses) -> List[TaskStatusResponse]:
+        """Statuses that arrived together (a status thread catching up after a slow write), in
+        arrival order. A scheduler with ``process_status_updates`` stores them in one transaction
+        (split where a status reads the stored history, ``status_reads_history``); the responses
+        are what ``task_status`` returns."""
+        batch_fn = getattr(self, "process_status_updates", None)
+        if batch_fn is None or len(statuses) < 2:
+            return [self.task_status(s) for s in statuses]
+        out: List[TaskStatusResponse] = []
+        run: List = []
+
+        def flush():
+            if not run:
+                return
+            try:
+                errors = batch_fn(run)
+            finally:
+                self.status_processed.set()
+            for st, err in zip(run, errors):
+                if err is None and self.reconciler is not None:
+                    try:
+                        self.reconciler.update(st)
+                    except Exception as e:  # noqa: BLE001
+                        err = e
+                out.append(TaskStatusResponse.processed() if err is None else self._status_failed(st, err))
+            run.clear()
+
+        for status in statuses:
+            self.launch_watchdog.update(status)
+            status = self._unknown_as_lost(status)
+            if self.status_reads_history(status):
+                # handled against the statuses before it already stored
+                flush()
+                out.append(self.task_status_processed(status))
+                continue
+            run.append(status)
+        flush()
+        return out
+
+    def status_reads_history(self, status) -> bool:
+        """Whether processing ``status`` reads the task's stored status (it is then processed
+        alone, after the statuses before it are stored)."""
+        return False
+
+    def task_status_processed(self, status) -> TaskStatusResponse:
+        """``task_status`` for a status that already went through the launch watchdog and the
+        TASK_UNKNOWN mapping."""
+        try:
+            self.process_status_update(status)
+            if self.reconciler is not None:
+                self.reconciler.update(status)
+        except Exception as e:  # noqa: BLE001
+            return self._status_failed(status, e)
+        finally:
+            self.status_processed.set()
+        return TaskStatusResponse.processed()
+
+    def _unknown_as_lost(self, status):
         if (self.unknown_as_lost and status.state == P.TASK_UNKNOWN
                 and status.reason == P.TaskStatus.REASON_RECONCILIATION):
             # The master has no record of the task (it never got the launch, or the agent was
@@ -139,20 +199,15 @@ class AbstractScheduler(MesosEventClient):
             lost.CopyFrom(status)
             lost.state = P.TASK_LOST
             lost.message = f"Unknown to the master on reconciliation: {status.message}"
-            status = lost
-        try:
-            self.process_status_update(status)
-            if self.reconciler is not None:
-                self.reconciler.update(status)
-        except StateStoreException as e:
+            return lost
+        return status
+
+    def _status_failed(self, status, e: BaseException) -> TaskStatusResponse:
+        if isinstance(e, StateStoreException):
             if e.reason == Reason.NOT_FOUND:
                 self.logger.info("Status for unknown task %s: %s", status.task_id.value, e)
                 return TaskStatusResponse.unknown_task()
-            self.logger.warning("Failed to update TaskStatus received from Mesos: %s", e)
-        except Exception as e:  # noqa: BLE001
-            self.logger.warning("Failed to update TaskStatus received from Mesos: %s", e)
-        finally:
-            self.status_processed.set()
+        self.logger.warning("Failed to update TaskStatus received from Mesos: %s", e)
         return TaskStatusResponse.processed()
 
     def awaiting_reconciliation(self) -> bool:

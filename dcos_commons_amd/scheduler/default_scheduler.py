@@ -19,6 +19,7 @@ from dcos_commons_amd.offer.resources import get_all_resources, get_resource_id,
 from dcos_commons_amd.offer.taskdata.labels import TaskLabelReader
 from dcos_commons_amd.scheduler.abstract_scheduler import AbstractScheduler
 from dcos_commons_amd.scheduler.decommission import DECOMMISSIONING_STATUS
+from dcos_commons_amd.scheduler.launch_pipeline import LaunchPipeline
 from dcos_commons_amd.scheduler.mesos_event_client import (
     ClientStatusResponse,
     OfferResources,
@@ -53,6 +54,11 @@ def _never_launched(info: P.TaskInfo, prev: Optional[P.TaskStatus], status: P.Ta
             and info.task_id.value == status.task_id.value
             and status.source == P.TaskStatus.SOURCE_MASTER and status.state in _NEVER_LAUNCHED_STATES
             and status.reason in _NEVER_LAUNCHED_REASONS and TaskLabelReader(info).is_launch_new_footprint())
+
+
+def _cfg_pipeline(scheduler_config) -> Optional[bool]:
+    fn = getattr(scheduler_config, "pipeline_launch_writes", None)
+    return fn() if callable(fn) else None
 
 
 def _is_working(plan, st: Optional[Status] = None) -> bool:
@@ -97,6 +103,7 @@ class DefaultScheduler(AbstractScheduler):
         self.recovery_plan_manager = next(pm for pm in pms if pm.get_plan().is_recovery_plan())
         self._deployment_completion_stored = False
         self._expected_ids_cache: Dict[str, tuple] = {}   # task name -> (TaskInfo bytes, resource IDs, perm-failed)
+        self._pipeline = None   # LaunchPipeline, False when launch records are written inline
         self.offer_outcome_tracker = None if namespace else OfferOutcomeTracker()
         self.offer_outcome_tracker_v2 = None if namespace else OfferOutcomeTrackerV2()
         if template_url_factory is None:
@@ -214,12 +221,37 @@ class DefaultScheduler(AbstractScheduler):
         # Launch streaming: each step's launch is recorded and sent to the master as soon as the
         # step is matched, so pods launch (and their agents start them) while later steps are
         # still being evaluated, instead of after the whole cycle.
-        def on_step(recs):
-            if not self._record(recs):
-                return []
-            launch_stream(recs)
+        pipeline = self._launch_pipeline()
+        if pipeline is None:
+            def on_step(recs):
+                if not self._record(recs):
+                    return []
+                launch_stream(recs)
+                return recs
+            return OfferResponse.processed(self.plan_scheduler.resource_offers(offers, steps, on_step),
+                                           streamed=True)
+
+        # ... and with a remote persister the records are written behind the evaluation
+        # (scheduler.launch_pipeline): ACCEPTs still follow their durable record, in step order
+        def on_step_pipelined(recs):
+            pipeline.submit(recs, launch_stream)
             return recs
-        return OfferResponse.processed(self.plan_scheduler.resource_offers(offers, steps, on_step), streamed=True)
+        try:
+            recs = self.plan_scheduler.resource_offers(offers, steps, on_step_pipelined)
+        finally:
+            failed = pipeline.drain()
+        if failed:
+            dropped = {id(r) for batch in failed for r in batch}
+            recs = [r for r in recs if id(r) not in dropped]
+        return OfferResponse.processed(recs, streamed=True)
+
+    def _launch_pipeline(self):
+        if self._pipeline is None:
+            on = _cfg_pipeline(self.scheduler_config)
+            if on is None:
+                on = getattr(self.state_store.persister, "remote", False)
+            self._pipeline = LaunchPipeline(self._record) if on else False
+        return self._pipeline or None
 
     def get_unexpected_resources(self, unused_offers) -> UnexpectedResourcesResponse:
         if not any(get_resource_id(r) is not None for offer in unused_offers for r in offer.resources):
@@ -273,6 +305,12 @@ class DefaultScheduler(AbstractScheduler):
         return UnexpectedResourcesResponse.processed(unexpected)
 
     def process_status_update(self, status: P.TaskStatus) -> None:
+        name, props = self._prepare_status(status)
+        self.state_store.store_status(name, status, props)
+        self._apply_status(status)
+
+    def _prepare_status(self, status: P.TaskStatus):
+        """What storing ``status`` needs: its task's name and the properties written with it."""
         info = state_store_utils.fetch_task_info(self.state_store, status)
         name = info.name
         if (self.unknown_as_lost and status.state in _NEVER_LAUNCHED_STATES
@@ -291,9 +329,37 @@ class DefaultScheduler(AbstractScheduler):
         if status.HasField("container_status") and any(
                 len(ni.ip_addresses) > 0 for ni in status.container_status.network_infos):
             props = {name + state_store_utils.PROPERTY_TASK_INFO_SUFFIX: status.SerializeToString()}
-        self.state_store.store_status(name, status, props)
+        return name, props
+
+    def _apply_status(self, status: P.TaskStatus) -> None:
         for pm in self.plan_coordinator.get_plan_managers():
             pm.update(status)
+
+    def status_reads_history(self, status: P.TaskStatus) -> bool:
+        # the never-launched check compares the status with the stored one
+        return self.unknown_as_lost and status.state in _NEVER_LAUNCHED_STATES
+
+    def process_status_updates(self, statuses) -> list:
+        """Statuses that arrived together: stored in one transaction, then applied to the plans in
+        arrival order. Returns each status's error (None when processed)."""
+        errors: list = [None] * len(statuses)
+        prepared = []
+        for i, status in enumerate(statuses):
+            try:
+                name, props = self._prepare_status(status)
+                prepared.append((i, name, props))
+            except Exception as e:  # noqa: BLE001
+                errors[i] = e
+        stored = self.state_store.store_statuses([(name, statuses[i], props) for i, name, props in prepared])
+        for (i, _, _), err in zip(prepared, stored):
+            if err is not None:
+                errors[i] = err
+                continue
+            try:
+                self._apply_status(statuses[i])
+            except Exception as e:  # noqa: BLE001
+                errors[i] = e
+        return errors
 
     def to_uninstall_scheduler(self):
         from dcos_commons_amd.scheduler.uninstall import UninstallScheduler

@@ -178,6 +178,12 @@ class MesosEventClient:
     def task_status(self, status: P.TaskStatus) -> TaskStatusResponse:
         raise NotImplementedError
 
+    def task_statuses(self, statuses: List[P.TaskStatus]) -> List[TaskStatusResponse]:
+        """Several statuses delivered together, in arrival order (no reference counterpart: the
+        reference handles one per driver callback). Clients that can store them in one
+        transaction override this."""
+        return [self.task_status(s) for s in statuses]
+
     def awaiting_reconciliation(self) -> bool:
         """True while explicit reconciliation has not finished. Offers are refused until then, so
         every status that arrives in that window may be the one that ends it, and the framework

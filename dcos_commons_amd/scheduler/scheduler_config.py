@@ -334,6 +334,15 @@ class SchedulerConfig:
         (reference: one batch of ACCEPTs at the end of the cycle)."""
         return self.env.get_optional_boolean("SDK_STREAM_LAUNCHES", True)
 
+    def pipeline_launch_writes(self) -> Optional[bool]:
+        """Overlap each streamed step's write-ahead record (its TaskInfos, in ZooKeeper) with the
+        evaluation of the next steps, writing what has queued up in one transaction and sending
+        the ACCEPTs in step order once it is durable (``SDK_PIPELINE_LAUNCH_WRITES``; unset: on
+        when the persister is remote). No reference counterpart: the reference records a cycle's
+        launches in one write after evaluating all of it, and its launches wait for that."""
+        v = self.env.get_optional("SDK_PIPELINE_LAUNCH_WRITES", "")
+        return None if v in ("", "auto") else v.lower() in ("1", "true", "yes")
+
     def launch_reconcile_s(self) -> float:
         """Explicitly reconcile a launch that still has no status after this many seconds, e.g.
         because its ACCEPT was lost (0 = reference behaviour: wait for the next scheduler

@@ -14,7 +14,10 @@ status whose TaskID differs from the stored one (other than the synthetic STAGIN
 """
 from __future__ import annotations
 
+import functools
 import logging
+import threading
+import weakref
 from typing import Collection, Dict, List, Optional, Tuple
 
 from dcos_commons_amd.mesos import protos as P
@@ -40,15 +43,43 @@ _NON_TERMINAL_OVERWRITE_STATES = frozenset(
     [P.TASK_LOST, P.TASK_GONE, P.TASK_DROPPED, P.TASK_UNKNOWN, P.TASK_UNREACHABLE])
 
 
+_UNSET = object()
+
+
 class StateStoreException(Exception):
     def __init__(self, reason: Reason, message: str = ""):
         super().__init__(f"{reason.value}: {message}")
         self.reason = reason
 
 
+_STATUS_LOCKS: "weakref.WeakKeyDictionary" = weakref.WeakKeyDictionary()
+_STATUS_LOCKS_GUARD = threading.Lock()
+
+
+def _status_lock(persister) -> threading.RLock:
+    """One lock per persister for every write that checks or replaces a TaskStatus: the status
+    thread's check-then-write (``store_status``) must not interleave with a launch record written
+    from another thread (``store_tasks``), or a late status of a replaced task could overwrite the
+    new task's STAGING status after passing its check against the old one."""
+    with _STATUS_LOCKS_GUARD:
+        lock = _STATUS_LOCKS.get(persister)
+        if lock is None:
+            lock = _STATUS_LOCKS[persister] = threading.RLock()
+        return lock
+
+
+def _status_write(fn):
+    @functools.wraps(fn)
+    def locked(self, *args, **kwargs):
+        with self._status_lock:
+            return fn(self, *args, **kwargs)
+    return locked
+
+
 class StateStore:
     def __init__(self, persister: Persister, namespace: Optional[str] = None, repair: bool = True):
         self.persister = persister
+        self._status_lock = _status_lock(persister)
         self.namespace = namespace or ""
         self.logger = logging.getLogger(__name__ + (f"({self.namespace})" if self.namespace else ""))
         self._tasks_root = get_service_namespaced_root_path(self.namespace, TASKS_ROOT_NAME)
@@ -107,6 +138,7 @@ class StateStore:
                 f"Property value length {len(value)} exceeds limit of {MAX_VALUE_LENGTH_BYTES} bytes.")
 
     # -- tasks ---------------------------------------------------------------------------
+    @_status_write
     def store_tasks(self, tasks: Collection[P.TaskInfo],
                     statuses: Collection[Tuple[str, P.TaskStatus]] = ()) -> None:
         """Stores TaskInfos in batches under 1 MB (StateStore.storeTasks). ``statuses`` (task
@@ -140,9 +172,11 @@ class StateStore:
         for name, st in checked:
             self.store_status(name, st)
 
-    def _check_status(self, task_name: str, status: P.TaskStatus) -> bool:
-        """The checks ``store_status`` applies before writing (raises on a rejected status)."""
-        current = self.fetch_status(task_name)
+    def _check_status(self, task_name: str, status: P.TaskStatus, current=_UNSET) -> bool:
+        """The checks ``store_status`` applies before writing (raises on a rejected status);
+        ``current`` is the task's status to check against (default: the stored one)."""
+        if current is _UNSET:
+            current = self.fetch_status(task_name)
         from dcos_commons_amd.offer.task_utils import is_terminal
 
         if current is not None and status.state in _NON_TERMINAL_OVERWRITE_STATES and is_terminal(current):
@@ -156,6 +190,7 @@ class StateStore:
                                       f"Dropping TaskStatus with unknown TaskID: {status.task_id.value}")
         return True
 
+    @_status_write
     def store_status(self, task_name: str, status: P.TaskStatus,
                      properties: Optional[Dict[str, bytes]] = None) -> None:
         """Stores ``status`` (StateStore.storeStatus). ``properties`` are written in the same
@@ -186,6 +221,50 @@ class StateStore:
             self.persister.set(self._task_status_path(task_name), data)
         except PersisterException as e:
             raise StateStoreException(e.reason, str(e)) from e
+
+    @_status_write
+    def store_statuses(self, items) -> List[Optional[StateStoreException]]:
+        """Stores several ``(task_name, status, properties)`` in one persister transaction (a status
+        thread that fell behind catches up with one ZooKeeper multi instead of a round trip per
+        status). Validation is per item, as in :meth:`store_status`; several statuses of one task
+        are checked in order, each against the one before it, and the last one is what ends up
+        stored, as storing them one by one would leave it. If the combined write fails, every item
+        is stored alone so one bad item cannot take the others with it. Returns each item's error
+        (None when stored)."""
+        errors: List[Optional[StateStoreException]] = [None] * len(items)
+        batch: Dict[str, bytes] = {}
+        latest: Dict[str, P.TaskStatus] = {}     # a later status of a task is checked against the earlier
+        for i, (name, status, props) in enumerate(items):
+            try:
+                self._check_status(name, status, latest[name] if name in latest else _UNSET)
+            except StateStoreException as e:
+                errors[i] = e
+                continue
+            latest[name] = status
+            for k, v in (props or {}).items():
+                try:
+                    self._validate_key(k)
+                    self._validate_value(v)
+                except StateStoreException as e:
+                    self.logger.warning("Not storing property '%s' with the status of %s: %s", k, name, e)
+                    continue
+                batch[self._property_path(k)] = v
+            batch[self._task_status_path(name)] = status.SerializeToString()
+        if not batch:
+            return errors
+        try:
+            self.persister.set_many(batch)
+            return errors
+        except PersisterException as e:
+            self.logger.warning("Failed to store %d statuses together (%s); storing them one at a time",
+                                len(items), e)
+        for i, (name, status, props) in enumerate(items):
+            if errors[i] is None:
+                try:
+                    self.store_status(name, status, props)
+                except StateStoreException as e:
+                    errors[i] = e
+        return errors
 
     def clear_task(self, task_name: str) -> None:
         try:

@@ -29,6 +29,12 @@ class PersisterException(Exception):
 
 
 class Persister(ABC):
+    @property
+    def remote(self) -> bool:
+        """Whether a write is a network round trip (ZooKeeper) rather than a local update:
+        the scheduler then overlaps its write-ahead launch records with step evaluation."""
+        return False
+
     @abstractmethod
     def get(self, path: str) -> Optional[bytes]:
         ...

@@ -62,6 +62,10 @@ class ZooKeeperPersister(Persister):
         self.client = client or new_client(connect, username, password, session_timeout_ms)
 
     # -- helpers ------------------------------------------------------------------------
+    @property
+    def remote(self) -> bool:
+        return True
+
     def _p(self, path: str) -> str:
         p = join_paths(self.root, path or "")
         while len(p) > 1 and p.endswith("/"):

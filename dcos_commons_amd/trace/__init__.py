@@ -51,7 +51,7 @@ _NULL = _NullSpan()
 
 
 class _Span:
-    __slots__ = ("tracer", "name", "cat", "args", "t0")
+    __slots__ = ("tracer", "name", "cat", "args", "t0", "c0")
 
     def __init__(self, tracer: "Tracer", name: str, cat: str, args: Dict[str, Any]):
         self.tracer = tracer
@@ -60,11 +60,15 @@ class _Span:
         self.args = args
 
     def __enter__(self):
+        self.c0 = time.thread_time_ns()
         self.t0 = time.perf_counter_ns()
         return self
 
     def __exit__(self, exc_type, exc, tb):
         t1 = time.perf_counter_ns()
+        # the thread's own CPU time inside the span: wall minus this is time spent waiting (I/O,
+        # locks, the interpreter lock held by another thread)
+        self.args["cpu_us"] = (time.thread_time_ns() - self.c0) // 1000
         if exc_type is not None:
             self.args["error"] = exc_type.__name__
         self.tracer._record(self.name, self.cat, self.t0, t1 - self.t0, self.args)
@@ -125,7 +129,9 @@ class Tracer:
         meta = [{"name": "thread_name", "ph": "M", "pid": _PID, "tid": t, "args": {"name": _thread_name(t)}}
                 for t in sorted(names)]
         return {"traceEvents": meta + evs, "displayTimeUnit": "ms",
-                "otherData": {"enabled": self.enabled, "dropped": self.dropped}}
+                "otherData": {"enabled": self.enabled, "dropped": self.dropped,
+                              # ts 0 on the host's monotonic clock: aligns traces of several processes
+                              "epoch_monotonic_ns": self._epoch_ns}}
 
     def summary(self) -> Dict[str, dict]:
         """Per-span-name count / total / mean / max in milliseconds (for benches and logs)."""
@@ -211,6 +217,10 @@ class TracingPersister(Persister):
 
     def __getattr__(self, item):  # PersisterCache.refresh(), backend-specific helpers
         return getattr(self.inner, item)
+
+    @property
+    def remote(self) -> bool:
+        return self.inner.remote
 
     def get(self, path: str) -> Optional[bytes]:
         with span("persister.get", "persister", path=path):

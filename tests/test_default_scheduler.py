@@ -649,3 +649,84 @@ def test_runner_checks_the_schema_version():
     builder = SchedulerBuilder(MINIMAL, CFG, persister)
     with pytest.raises(Exception, match="123|[Ss]chema"):
         SchedulerRunner.from_scheduler_builder(builder).run()
+
+
+# ---------------------------------------------------------------------------------------
+# Status updates delivered together (the v1 driver hands over every UPDATE it read at once)
+
+
+class _CountingPersister(MemPersister):
+    def __init__(self):
+        super().__init__()
+        self.writes = 0
+        self.fail_many = False
+
+    def set(self, path, data):
+        self.writes += 1
+        super().set(path, data)
+
+    def set_many(self, path_bytes):
+        self.writes += 1
+        if self.fail_many and len(path_bytes) > 2:
+            from dcos_commons_amd.storage.persister import PersisterException, Reason
+            raise PersisterException(Reason.STORAGE_ERROR, "injected")
+        super().set_many(path_bytes)
+
+
+def _installed(drv, persister):
+    hh = Harness.__new__(Harness)
+    hh.drv, hh.persister = drv, persister
+    FrameworkStore(persister).store_framework_id(U.FRAMEWORK_ID)
+    hh.build(service_spec(POD_A, POD_B))
+    return hh, hh.install()
+
+
+def _stored(persister):
+    store = StateStore(persister)
+    return {n: store.fetch_status(n).state for n in store.fetch_task_names()}, \
+        {k: store.fetch_property(k) for k in store.fetch_property_keys()}
+
+
+def test_status_batch_stores_once_and_matches_one_by_one(env):
+    one, ids = _installed(env, _CountingPersister())
+    batch, ids_b = _installed(env, _CountingPersister())
+    seq = [(0, P.TASK_RUNNING), (1, P.TASK_FAILED), (2, P.TASK_RUNNING), (2, P.TASK_KILLED),
+           (0, P.TASK_RUNNING)]
+    w0 = one.persister.writes
+    for i, st in seq:
+        one.scheduler.task_status(task_status(ids[i], st))
+    assert one.persister.writes - w0 == len(seq)
+    w0 = batch.persister.writes
+    resps = batch.scheduler.task_statuses([task_status(ids_b[i], st) for i, st in seq])
+    assert batch.persister.writes - w0 == 1          # one transaction for the five updates
+    assert [r.result.value for r in resps] == ["PROCESSED"] * len(seq)
+    states_1, props_1 = _stored(one.persister)
+    states_b, props_b = _stored(batch.persister)
+    assert states_1 == states_b == {"POD-A-0-A": P.TASK_RUNNING, "POD-B-0-B": P.TASK_FAILED,
+                                    "POD-B-1-B": P.TASK_KILLED}
+    def norm(props):
+        return {k: P.TaskStatus.FromString(v).state if k.endswith(":task-status") else v for k, v in props.items()}
+    assert norm(props_1) == norm(props_b)
+    assert one.statuses("recovery") == batch.statuses("recovery")
+    assert one.statuses() == batch.statuses() == [Status.COMPLETE] * 3
+
+
+def test_status_batch_checks_each_status_against_the_one_before(env):
+    hh, ids = _installed(env, _CountingPersister())
+    bogus = P.TaskID(value="POD-A-0-A__not-launched")
+    resps = hh.scheduler.task_statuses([task_status(ids[0], P.TASK_FAILED), task_status(ids[0], P.TASK_UNREACHABLE),
+                                        task_status(bogus, P.TASK_RUNNING), task_status(ids[1], P.TASK_RUNNING)])
+    assert [r.result.value for r in resps] == ["PROCESSED", "PROCESSED", "UNKNOWN_TASK", "PROCESSED"]
+    states, _ = _stored(hh.persister)
+    # UNREACHABLE after FAILED in the same batch is dropped, as it is when stored one by one
+    assert states["POD-A-0-A"] == P.TASK_FAILED and states["POD-B-0-B"] == P.TASK_RUNNING
+
+
+def test_status_batch_falls_back_to_one_write_each(env):
+    hh, ids = _installed(env, _CountingPersister())
+    hh.persister.fail_many = True
+    w0 = hh.persister.writes
+    hh.scheduler.task_statuses([task_status(ids[i], P.TASK_RUNNING) for i in range(3)])
+    assert hh.persister.writes - w0 == 1 + 3
+    states, _ = _stored(hh.persister)
+    assert set(states.values()) == {P.TASK_RUNNING}

@@ -37,6 +37,31 @@ def test_recordio_roundtrip_and_partial_feeds():
         list(recordio.iter_records(lambda n: next(bad)))
 
 
+def _chunked(payload: bytes, sizes, ext=b"") -> bytes:
+    out, i = b"", 0
+    for n in sizes:
+        out += b"%x%s\r\n" % (n, ext) + payload[i:i + n] + b"\r\n"
+        i += n
+    return out + b"0\r\n\r\n"
+
+
+def test_chunked_decoder_returns_everything_that_arrived():
+    payload = b"".join(recordio.encode(r) for r in (b"a" * 300, b"", b"event\r\n3"))
+    for ext in (b"", b";name=value"):
+        wire = _chunked(payload, [1, 17, 0x100, len(payload) - 0x112], ext)
+        for step in (1, 2, 5, 64, len(wire)):
+            dec, out = recordio.ChunkedDecoder(), b""
+            for i in range(0, len(wire), step):
+                out += dec.feed(wire[i:i + step])
+            assert out == payload and dec.done
+    dec = recordio.ChunkedDecoder()
+    assert dec.feed(_chunked(b"xy", [2]) + b"ignored after the last chunk") == b"xy" and dec.done
+    with pytest.raises(recordio.RecordIOError):
+        recordio.ChunkedDecoder().feed(b"zz\r\n")
+    with pytest.raises(recordio.RecordIOError):
+        recordio.ChunkedDecoder().feed(b"2\r\nabXY")
+
+
 class Recorder:
     def __init__(self):
         self.events = []
@@ -429,3 +454,39 @@ def test_async_calls_are_sent_in_order_and_failures_are_logged(caplog):
         d.stop()
         hm.stop()
         lm.shutdown()
+
+
+def test_updates_read_together_reach_the_scheduler_together(cluster):
+    """UPDATE events that queue up while the scheduler is busy are handed to ``status_updates``
+    in one call, in stream order (the scheduler stores them in one transaction)."""
+    lm, hm = cluster
+    gate = threading.Event()
+
+    class Batching(Recorder):
+        def status_update(self, d, st):
+            gate.wait(10)               # busy: the next updates pile up on the stream
+            self._add("update", st)
+
+        def status_updates(self, d, sts):
+            self._add("batch", [s.task_id.value for s in sts])
+            for s in sts:
+                self._add("update", s)
+
+    rec = Batching()
+    d = V1HttpSchedulerDriver(hm.url, rec, P.FrameworkInfo(name="fw", role="r", user="u"))
+    d.start()
+    try:
+        rec.wait_for("registered")
+        d.reconcile_tasks([P.TaskStatus(task_id=P.TaskID(value="first"), state=P.TASK_RUNNING)])
+        time.sleep(0.2)                 # the stream thread is now inside status_update("first")
+        names = [f"t{i}" for i in range(6)]
+        d.reconcile_tasks([P.TaskStatus(task_id=P.TaskID(value=n), state=P.TASK_RUNNING) for n in names])
+        time.sleep(0.3)
+        gate.set()
+        ups = rec.wait_for("update", 1 + len(names))
+        assert [u[1].task_id.value for u in ups] == ["first"] + names
+        batches = [e[1] for e in rec.events if e[0] == "batch"]
+        assert batches and max(len(b) for b in batches) > 1
+        assert [n for b in batches for n in b] == names[len(names) - sum(len(b) for b in batches):]
+    finally:
+        d.stop()

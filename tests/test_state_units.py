@@ -247,6 +247,47 @@ def test_terminal_task_is_not_overwritten_by_a_late_lost_like_status(store, late
     assert store.fetch_status(TASK).state == P.TASK_FINISHED
 
 
+def test_late_status_of_a_replaced_task_cannot_overwrite_the_relaunch_record():
+    """A status of the old task, checked against the old task's status while another thread
+    records the relaunch (new TaskInfo + STAGING), must not land on top of that record: the
+    check and the write of a status and a launch record's write do not interleave."""
+    import threading
+
+    wrote_old = threading.Event()
+    release = threading.Event()
+
+    class SlowStatusWrites(MemPersister):
+        def set(self, path, data):
+            if path.endswith("TaskStatus") and not wrote_old.is_set():
+                wrote_old.set()
+                release.wait(5)          # the old task's status is checked and about to be written
+            super().set(path, data)
+
+    store = StateStore(SlowStatusWrites())
+    old = info()
+    store.store_tasks([old], [(TASK, status(old.task_id, P.TASK_STAGING))])
+    store.persister.set("ready", b"")
+    new = info(tid=to_task_id(SERVICE, TASK))
+    errors = []
+
+    def late_status():
+        try:
+            store.store_status(TASK, status(old.task_id, P.TASK_LOST))
+        except StateStoreException as e:
+            errors.append(e)
+    t1 = threading.Thread(target=late_status)
+    t1.start()
+    assert wrote_old.wait(5)
+    t2 = threading.Thread(target=lambda: store.store_tasks([new], [(TASK, status(new.task_id, P.TASK_STAGING))]))
+    t2.start()
+    t2.join(0.2)                        # the relaunch record waits for the status write in flight
+    release.set()
+    t1.join(5)
+    t2.join(5)
+    assert store.fetch_status(TASK).task_id == new.task_id
+    assert store.fetch_status(TASK).state == P.TASK_STAGING
+
+
 def test_terminal_task_accepts_a_new_terminal_state(store):
     t = info()
     store.store_tasks([t])
