@@ -225,14 +225,18 @@ def main(argv: Optional[List[str]] = None) -> int:
     ap.add_argument("--allocation-interval", type=float, default=1.0)
     ap.add_argument("--probe-service", action="store_true",
                     help="run the node's GPU readiness service; the default check becomes amd-gpu-ready")
+    ap.add_argument("--scheduler-env", action="append", default=[], metavar="KEY=VALUE",
+                    help="extra environment for the scheduler process (repeatable), e.g. for same-box A/Bs")
     args = ap.parse_args(argv)
     if args.probe_service and args.probe_cmd == DEFAULT_PROBE:
         from dcos_commons_amd.ops.probe_service import CLIENT_BINARY
 
         args.probe_cmd = CLIENT_BINARY
     logging.basicConfig(level=logging.ERROR)
+    env = dict(PROFILES[args.profile])
+    env.update(kv.split("=", 1) for kv in args.scheduler_env)
     bench = ClusterBench(args.agents, args.executor, args.probe_cmd, args.allocation_interval,
-                         profile_env=PROFILES[args.profile], probe_service=args.probe_service)
+                         profile_env=env, probe_service=args.probe_service)
     served = None
     try:
         for _ in range(args.warmup):
@@ -250,6 +254,7 @@ def main(argv: Optional[List[str]] = None) -> int:
     print(json.dumps({"bench": "cluster", "agents": args.agents, "pods": args.agents, "cycles": args.cycles,
                       "executor": args.executor, "probe_cmd": args.probe_cmd, "profile": args.profile,
                       "allocation_interval_s": args.allocation_interval, "probe_service": args.probe_service,
+                      "scheduler_env": dict(kv.split("=", 1) for kv in args.scheduler_env),
                       "probe_service_checks": served,
                       "deploy_s": stat("deploy_s"), "mttr_restart_s": stat("mttr_restart_s"),
                       "mttr_replace_s": stat("mttr_replace_s"),
