@@ -38,6 +38,14 @@ def get_task_environment(service_name: str, pod_instance: PodInstance, task_spec
     env: Dict[str, str] = {}
     if task_spec.command is not None:
         env.update(task_spec.command.env)
+    env.update(_instance_environment(service_name, pod_instance, task_spec, scheduler_config))
+    return dict(sorted(env.items()))
+
+
+def _instance_environment(service_name: str, pod_instance: PodInstance, task_spec: TaskSpec,
+                          scheduler_config) -> Dict[str, str]:
+    """The variables every task gets on top of its spec's ``env`` (PodInfoBuilder.getTaskEnvironment)."""
+    env: Dict[str, str] = {}
     task_name = f"{pod_instance.name}-{task_spec.name}"
     env[L.POD_INSTANCE_INDEX_TASKENV] = str(pod_instance.index)
     env[L.FRAMEWORK_NAME_TASKENV] = service_name
@@ -49,7 +57,18 @@ def get_task_environment(service_name: str, pod_instance: PodInstance, task_spec
     env[task_name] = "true"
     env[L.PLACEMENT_REFERENCED_REGION_ENV] = str(placement.references_region(pod_instance.pod)).lower()
     env[L.PLACEMENT_REFERENCED_ZONE_ENV] = str(placement.references_zone(pod_instance.pod)).lower()
-    return dict(sorted(env.items()))
+    return env
+
+
+def _environment_bytes(service_name: str, pod_instance: PodInstance, task_spec: TaskSpec, scheduler_config,
+                       more: Optional[Dict[str, str]] = None) -> bytes:
+    """``get_task_environment`` (plus ``more``) as a serialized, name-sorted ``Environment``, from
+    the spec env's cached pre-encoded template and the per-instance variables."""
+    extra = _instance_environment(service_name, pod_instance, task_spec, scheduler_config)
+    if more:
+        extra.update(more)
+    static = task_spec.command.environment if task_spec.command is not None else ()
+    return L.env_template(static).encode(extra)
 
 
 def config_template_download_path(config: ConfigFileSpec) -> str:
@@ -175,18 +194,16 @@ class PodInfoBuilder:
         w.set_additional_labels(ts.labels)
         w.apply()
         # the command, health check and readiness check all start from the same task environment
-        env_map = get_task_environment(service_name, pi, ts, scheduler_config)
-        base_env = L.env_from_map(env_map)
+        base_env = P.Environment()
+        base_env.MergeFromString(_environment_bytes(service_name, pi, ts, scheduler_config))
         if ts.command is not None:
             cmd = t.command
             if ts.config_files:
                 # EnvUtils.withEnvVar per config file (PodInfoBuilder.java:279-283): keyed by name,
-                # sorted; applied to the map in one pass rather than re-sorting the proto per file
-                cmd_map = dict(env_map)
-                for config in ts.config_files:
-                    cmd_map[CONFIG_TEMPLATE_KEY_FORMAT % L.to_env_name(config.name)] = \
-                        f"{config_template_download_path(config)},{config.relative_path}"
-                cmd.environment.CopyFrom(L.env_from_map(cmd_map))
+                # sorted; merged in one pass rather than re-sorting the proto per file
+                more = {CONFIG_TEMPLATE_KEY_FORMAT % L.to_env_name(config.name):
+                        f"{config_template_download_path(config)},{config.relative_path}" for config in ts.config_files}
+                cmd.environment.MergeFromString(_environment_bytes(service_name, pi, ts, scheduler_config, more))
             else:
                 cmd.environment.CopyFrom(base_env)
             if override == GoalStateOverride.PAUSED:

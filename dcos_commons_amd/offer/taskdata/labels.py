@@ -9,6 +9,7 @@ rest of the scheduler -- and the checkpointed state -- relies on.
 from __future__ import annotations
 
 import base64
+import bisect
 import functools
 import re
 import uuid
@@ -421,6 +422,55 @@ def env_bytes_from_map(m: Dict[str, str]) -> bytes:
     """Serialized ``Environment`` of ``m`` with variables sorted by name (EnvUtils.toProto over a
     TreeMap); ``MergeFromString`` it into an empty environment field."""
     return b"".join([_env_entry(k, m[k]) for k in sorted(m)])
+
+
+class EnvTemplate:
+    """A task spec's own environment, sorted and encoded once; ``encode(extra)`` merges a few
+    per-instance variables (pod index, task name, config template paths) into it in name order,
+    copying the static runs between them as byte slices. The result is byte-identical to
+    ``env_bytes_from_map({**static, **extra})`` at the cost of the extra keys alone (a reference
+    hdfs task carries ~320 static variables and ~11 per-instance ones)."""
+
+    __slots__ = ("keys", "blob", "offsets")
+
+    def __init__(self, static: Dict[str, str]):
+        self.keys = sorted(static)
+        entries = [_env_entry(k, static[k]) for k in self.keys]
+        self.blob = b"".join(entries)
+        offsets = [0]
+        for e in entries:
+            offsets.append(offsets[-1] + len(e))
+        self.offsets = offsets
+
+    def encode(self, extra: Dict[str, str]) -> bytes:
+        keys, offsets, blob = self.keys, self.offsets, self.blob
+        parts = []
+        pos = 0
+        for k in sorted(extra):
+            i = bisect.bisect_left(keys, k, pos)
+            parts.append(blob[offsets[pos]:offsets[i]])
+            parts.append(_env_entry(k, extra[k]))
+            pos = i + 1 if i < len(keys) and keys[i] == k else i   # an extra value replaces the static one
+        parts.append(blob[offsets[pos]:])
+        return b"".join(parts)
+
+
+_ENV_TEMPLATES: Dict[int, tuple] = {}   # id(spec environment) -> (spec environment, EnvTemplate)
+_ENV_TEMPLATES_MAX = 1024
+
+
+def env_template(static) -> EnvTemplate:
+    """The (cached) template of a spec's environment: a ``CommandSpec.environment`` tuple of
+    (name, value) pairs, or a mapping. Keyed by that object, which the cache keeps alive so its
+    id cannot be reused; spec environments are immutable."""
+    hit = _ENV_TEMPLATES.get(id(static))
+    if hit is not None and hit[0] is static:
+        return hit[1]
+    if len(_ENV_TEMPLATES) >= _ENV_TEMPLATES_MAX:
+        _ENV_TEMPLATES.clear()
+    t = EnvTemplate(static if isinstance(static, dict) else dict(static))
+    _ENV_TEMPLATES[id(static)] = (static, t)
+    return t
 
 
 def env_from_map(m: Dict[str, str]) -> P.Environment:

@@ -49,11 +49,48 @@ def _construct_mapping(loader, node, deep=False):
 _StrictLoader.add_constructor(yaml.resolver.BaseResolver.DEFAULT_MAPPING_TAG, _construct_mapping)
 
 
+_STR_TAG = "tag:yaml.org,2002:str"
+_MAP_TAG = yaml.resolver.BaseResolver.DEFAULT_MAPPING_TAG
+_SEQ_TAG = yaml.resolver.BaseResolver.DEFAULT_SEQUENCE_TAG
+_MERGE_TAG = "tag:yaml.org,2002:merge"
+
+
+def _to_python(loader, node) -> Any:
+    """The safe constructor's result for ``node``, with the common cases -- string scalars,
+    plain mappings and sequences -- converted directly. PyYAML's constructor spends most of a
+    service spec's load in per-node bookkeeping (a generator per mapping, recursion state); a
+    rendered svc.yml is almost all strings, maps and lists. Anything else (ints, bools, nulls,
+    merge keys, explicit tags) goes through the loader's own constructors, so the results are
+    the same, duplicate keys included."""
+    tag = node.tag
+    if tag == _STR_TAG and isinstance(node, yaml.ScalarNode):
+        return node.value
+    if tag == _MAP_TAG and isinstance(node, yaml.MappingNode):
+        out = {}
+        for key_node, value_node in node.value:
+            if key_node.tag == _MERGE_TAG:
+                return loader.construct_object(node, deep=True)   # `<<:` merges: the loader's flattening
+            key = _to_python(loader, key_node)
+            if not isinstance(key, str):
+                key = str(key)
+            if key in out:
+                raise RawSpecError(f"Duplicate field '{key}' (line {key_node.start_mark.line + 1})")
+            out[key] = _to_python(loader, value_node)
+        return out
+    if tag == _SEQ_TAG and isinstance(node, yaml.SequenceNode):
+        return [_to_python(loader, n) for n in node.value]
+    return loader.construct_object(node, deep=True)
+
+
 def load_yaml_strict(text: str) -> Any:
+    loader = _StrictLoader(text)
     try:
-        return yaml.load(text, Loader=_StrictLoader)  # noqa: S506 - SafeLoader subclass
+        node = loader.get_single_node()
+        return None if node is None else _to_python(loader, node)
     except yaml.YAMLError as e:
         raise RawSpecError(f"Invalid YAML: {e}") from e
+    finally:
+        loader.dispose()
 
 
 # Allowed keys per node type (Jackson FAIL_ON_UNKNOWN_PROPERTIES).

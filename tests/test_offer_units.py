@@ -447,3 +447,23 @@ def test_wire_template_reservations_equal_the_builder(refined, pre_reserved, nam
         pid = get_persistence_id(v)
         assert get_resource_id(v) == rid and pid and pid != rid
         assert v == ResourceBuilder.from_volume_spec(vol, rid, namespace, pid, None, None, "fw-id").build()
+
+
+def test_env_template_merges_like_a_sorted_map():
+    """``labels.EnvTemplate`` (a task spec's environment encoded once; per-instance variables
+    merged in name order as byte slices) is byte-identical to encoding the merged, sorted map."""
+    import random
+
+    from dcos_commons_amd.offer.taskdata import labels as L
+
+    rnd = random.Random(7)
+    names = [f"{rnd.choice('ABCDEFGHIJ')}{rnd.choice('_XYZ0')}{i}" for i in range(60)]
+    for trial in range(200):
+        static = {n: f"v{rnd.randrange(5)}" for n in rnd.sample(names, rnd.randrange(0, 40))}
+        extra = {n: f"x{rnd.randrange(5)}" for n in rnd.sample(names + ["AAA", "zzz", "M"], rnd.randrange(0, 12))}
+        got = L.EnvTemplate(static).encode(extra)
+        assert got == L.env_bytes_from_map({**static, **extra}), (static, extra)
+    assert L.env_template(static) is L.env_template(static)      # cached per spec map
+    env = P.Environment()
+    env.MergeFromString(L.EnvTemplate({"B": "2", "D": "4"}).encode({"A": "1", "D": "x", "E": "5"}))
+    assert [(v.name, v.value) for v in env.variables] == [("A", "1"), ("B", "2"), ("D", "x"), ("E", "5")]
