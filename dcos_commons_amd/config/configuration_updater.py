@@ -114,8 +114,15 @@ class DefaultConfigurationUpdater:
         except Exception:  # noqa: BLE001
             self.logger.exception("Unable to diff target config %s against the new config", old_id)
 
-    def _needs_config_update(self, info: P.TaskInfo, target, task_config) -> bool:
-        if target == task_config:
+    def _needs_config_update(self, info: P.TaskInfo, target, task_config, memo: Optional[dict] = None) -> bool:
+        """``memo`` (one per cleanup pass): the spec and pod comparisons depend only on the two
+        configs and the pod type, so the tasks of a pod type are compared once, not per task
+        (a reference hdfs spec compares ~320-variable environments)."""
+        memo = {} if memo is None else memo
+        same = memo.get(id(task_config))
+        if same is None:
+            same = memo[id(task_config)] = target == task_config
+        if same:
             return False
         try:
             r = TaskLabelReader(info)
@@ -125,14 +132,17 @@ class DefaultConfigurationUpdater:
             return True
         if perm_failed:
             return False
-        tp, op = target.pod(pod_type), task_config.pod(pod_type)
-        if tp is None or op is None:
-            return True
-        return not pods_match(tp, op)
+        key = (id(task_config), pod_type)
+        match = memo.get(key)
+        if match is None:
+            tp, op = target.pod(pod_type), task_config.pod(pod_type)
+            match = memo[key] = tp is not None and op is not None and pods_match(tp, op)
+        return not match
 
     def _cleanup(self, target, target_id) -> None:
         to_update: List[P.TaskInfo] = []
         needed = {target_id}
+        memo: dict = {}
         for info in self.state_store.fetch_tasks():
             try:
                 cid = TaskLabelReader(info).get_target_configuration()
@@ -145,7 +155,7 @@ class DefaultConfigurationUpdater:
             except ConfigStoreException:
                 needed.add(cid)
                 continue
-            if not self._needs_config_update(info, target, task_config):
+            if not self._needs_config_update(info, target, task_config, memo):
                 c = P.TaskInfo()
                 c.CopyFrom(info)
                 TaskLabelWriter(c).set_target_configuration(target_id).apply()

@@ -170,7 +170,7 @@ class OfferEvaluator:
         if not offers:
             return []  # nothing to match: the pipeline would be built for no offer
         if all_tasks is None:
-            all_tasks = {t.name: t for t in self.state_store.fetch_tasks()}
+            all_tasks = {t.name: t for t in self.state_store.fetch_tasks_shared()}
         pi = requirement.pod_instance
         this_pod = {}
         for name in task_utils.get_task_names(pi):

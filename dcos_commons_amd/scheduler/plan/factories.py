@@ -49,7 +49,7 @@ class DefaultStepFactory:
             infos = []
             for t in pod_instance.pod.tasks:
                 if t.name in tasks_to_launch:
-                    info = self.state_store.fetch_task(f"{pod_instance.name}-{t.name}")
+                    info = self.state_store.fetch_task_shared(f"{pod_instance.name}-{t.name}")
                     if info is not None:
                         infos.append(info)
             status = Status.PENDING if not infos else self._status(pod_instance, infos)

@@ -37,7 +37,7 @@ class PlanScheduler:
         available = list(offers)
         # Read the stored task set once per cycle; the TaskInfos of each matched step are merged
         # into it, so later steps see the pods placed earlier in this cycle.
-        all_tasks = {t.name: t for t in self.state_store.fetch_tasks()} if steps else {}
+        all_tasks = {t.name: t for t in self.state_store.fetch_tasks_shared()} if steps else {}
         for step in steps:
             recs = self._step_offers(available, step, all_tasks)
             if recs:

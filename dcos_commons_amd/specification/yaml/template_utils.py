@@ -18,6 +18,7 @@ The same grammar is implemented in C++ for the in-task ``bootstrap`` helper
 """
 from __future__ import annotations
 
+import collections.abc
 import re
 from dataclasses import dataclass
 from typing import Any, Dict, List, Mapping, Optional, Tuple
@@ -175,6 +176,12 @@ def _parse(tokens, i=0, closing: Optional[str] = None):
 _MISSING = object()
 
 
+def _is_map(x) -> bool:
+    # a plain dict first: typing.Mapping's isinstance goes through the ABC machinery on every
+    # variable of every template (~200 lookups in an hdfs-site.xml)
+    return type(x) is dict or isinstance(x, collections.abc.Mapping)
+
+
 def _lookup(stack: List[Any], name: str):
     if name == ".":
         return stack[-1]
@@ -182,14 +189,14 @@ def _lookup(stack: List[Any], name: str):
         # jmustache (non-standards mode) tries the whole key first: Universe options are
         # flattened to keys like "service.user" (CosmosRenderer.flattenPropertyTree).
         for ctx in reversed(stack):
-            if isinstance(ctx, Mapping) and name in ctx:
+            if _is_map(ctx) and name in ctx:
                 return ctx[name]
     parts = name.split(".")
     for ctx in reversed(stack):
-        if isinstance(ctx, Mapping) and parts[0] in ctx:
+        if _is_map(ctx) and parts[0] in ctx:
             v = ctx[parts[0]]
             for p in parts[1:]:
-                if isinstance(v, Mapping) and p in v:
+                if _is_map(v) and p in v:
                     v = v[p]
                 else:
                     return _MISSING
@@ -237,7 +244,7 @@ def _render(nodes, stack, out: List[str], missing: List[MissingValue]) -> None:
             if isinstance(v, (list, tuple)):
                 for item in v:
                     _render(children, stack + [item], out, missing)
-            elif isinstance(v, Mapping):
+            elif _is_map(v):
                 _render(children, stack + [v], out, missing)
             else:
                 _render(children, stack, out, missing)

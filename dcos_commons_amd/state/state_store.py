@@ -16,6 +16,7 @@ from __future__ import annotations
 
 import functools
 import logging
+import os
 import threading
 import weakref
 from typing import Collection, Dict, List, Optional, Tuple
@@ -52,6 +53,7 @@ class StateStoreException(Exception):
         self.reason = reason
 
 
+_DEBUG_SHARED = os.environ.get("SDK_DEBUG_SHARED_TASKS", "") not in ("", "0", "false")
 _STATUS_LOCKS: "weakref.WeakKeyDictionary" = weakref.WeakKeyDictionary()
 _STATUS_LOCKS_GUARD = threading.Lock()
 
@@ -80,6 +82,7 @@ class StateStore:
     def __init__(self, persister: Persister, namespace: Optional[str] = None, repair: bool = True):
         self.persister = persister
         self._status_lock = _status_lock(persister)
+        self._shared: Dict[str, tuple] = {}   # task name -> (TaskInfo bytes, parsed TaskInfo)
         self.namespace = namespace or ""
         self.logger = logging.getLogger(__name__ + (f"({self.namespace})" if self.namespace else ""))
         self._tasks_root = get_service_namespaced_root_path(self.namespace, TASKS_ROOT_NAME)
@@ -312,6 +315,57 @@ class StateStore:
                 raise StateStoreException(Reason.SERIALIZATION_ERROR, str(e)) from e
             out.append(t)
         return out
+
+    def fetch_tasks_shared(self) -> List[P.TaskInfo]:
+        """``fetch_tasks`` for read-only callers (the offer cycle's task map): a task whose stored
+        bytes did not change since the last call is returned as the same parsed object instead of
+        being parsed again (a reference hdfs TaskInfo is 16-32 KB: its environment three times
+        over). Callers must not modify the returned TaskInfos. With ``SDK_DEBUG_SHARED_TASKS``
+        set (the test suite sets it) every call first checks that no cached TaskInfo was
+        modified since it was handed out."""
+        cache = self._shared
+        out = []
+        raw = self.fetch_tasks_bytes()
+        for name, data in raw.items():
+            hit = cache.get(name)
+            if hit is not None and (hit[0] is data or hit[0] == data):
+                if _DEBUG_SHARED and hit[1].SerializeToString() != hit[0]:
+                    raise AssertionError(f"a caller modified the shared TaskInfo of {name}")
+                out.append(hit[1])
+                continue
+            t = P.TaskInfo()
+            try:
+                t.ParseFromString(data)
+            except Exception as e:  # noqa: BLE001
+                raise StateStoreException(Reason.SERIALIZATION_ERROR, str(e)) from e
+            cache[name] = (data, t)
+            out.append(t)
+        if len(cache) > len(raw):
+            for gone in set(cache) - set(raw):
+                del cache[gone]
+        return out
+
+    def fetch_task_shared(self, task_name: str) -> Optional[P.TaskInfo]:
+        """``fetch_task`` for read-only callers, from the same cache as ``fetch_tasks_shared`` (the
+        plans built at a scheduler start read the same tasks once per plan that has a step for
+        them). Callers must not modify the returned TaskInfo."""
+        data = self.fetch_task_bytes(task_name)
+        if data is None:
+            return None
+        hit = self._shared.get(task_name)
+        if hit is not None and (hit[0] is data or hit[0] == data):
+            if _DEBUG_SHARED and hit[1].SerializeToString() != hit[0]:
+                raise AssertionError(f"a caller modified the shared TaskInfo of {task_name}")
+            return hit[1]
+        if not data:
+            raise StateStoreException(Reason.SERIALIZATION_ERROR, f"Empty TaskInfo for TaskName: {task_name}")
+        t = P.TaskInfo()
+        try:
+            t.ParseFromString(data)
+        except Exception as e:  # noqa: BLE001
+            raise StateStoreException(Reason.SERIALIZATION_ERROR, str(e)) from e
+        self._shared[task_name] = (data, t)
+        return t
 
     def fetch_task_bytes(self, task_name: str) -> Optional[bytes]:
         """The serialized TaskInfo as stored (None when absent), for callers that memoize what

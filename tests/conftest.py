@@ -3,6 +3,10 @@ import sys
 
 import pytest
 
+# every offer cycle in the suite checks that no caller modified a shared (read-only) TaskInfo
+# (StateStore.fetch_tasks_shared); set before the package is imported
+os.environ.setdefault("SDK_DEBUG_SHARED_TASKS", "1")
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)

@@ -431,3 +431,29 @@ def test_status_is_stored_even_when_its_property_is_not(store, persister):
     st2 = status(t.task_id, P.TASK_FAILED)
     flaky.store_status(TASK, st2, {TASK + ":task-status": st2.SerializeToString()})
     assert flaky.fetch_status(TASK) == st2
+
+
+def test_fetch_tasks_shared_reuses_unchanged_tasks(store):
+    a, b = info("a"), info("b")
+    store.store_tasks([a, b])
+    first = {t.name: t for t in store.fetch_tasks_shared()}
+    again = {t.name: t for t in store.fetch_tasks_shared()}
+    assert first["a"] is again["a"] and first["b"] is again["b"]
+    changed = info("a")
+    changed.labels.labels.add(key="k", value="v")
+    store.store_tasks([changed])
+    third = {t.name: t for t in store.fetch_tasks_shared()}
+    assert third["a"] is not first["a"] and third["a"] == changed and third["b"] is first["b"]
+    store.clear_task("b")
+    assert [t.name for t in store.fetch_tasks_shared()] == ["a"] and "b" not in store._shared
+
+
+def test_fetch_tasks_shared_detects_a_caller_that_modified_a_task(store, monkeypatch):
+    from dcos_commons_amd.state import state_store as SS
+
+    monkeypatch.setattr(SS, "_DEBUG_SHARED", True)
+    store.store_tasks([info("a")])
+    t = store.fetch_tasks_shared()[0]
+    t.labels.labels.add(key="oops", value="1")
+    with pytest.raises(AssertionError):
+        store.fetch_tasks_shared()
