@@ -141,14 +141,14 @@ class StateStore:
                 f"Property value length {len(value)} exceeds limit of {MAX_VALUE_LENGTH_BYTES} bytes.")
 
     # -- tasks ---------------------------------------------------------------------------
-    @_status_write
     def store_tasks(self, tasks: Collection[P.TaskInfo],
                     statuses: Collection[Tuple[str, P.TaskStatus]] = ()) -> None:
         """Stores TaskInfos in batches under 1 MB (StateStore.storeTasks). ``statuses`` (task
         name, status) are checked as ``store_status`` checks them and, when the TaskInfos fit one
         batch, written in that same transaction (a launch record is one ZooKeeper multi instead of
-        one for the TaskInfos and one per status); otherwise they follow, one write each."""
-        checked = [(name, st) for name, st in statuses if self._check_status(name, st)]
+        one for the TaskInfos and one per status); otherwise they follow, one write each. The
+        TaskInfos are serialized before the status lock is taken: it covers only the checks and
+        the writes."""
         batches: List[Dict[str, bytes]] = []
         sizes: List[int] = []
         for t in tasks:
@@ -161,19 +161,21 @@ class StateStore:
             sizes[-1] += len(data)
         if len(batches) > 1:
             self.logger.warning("Grouped %d TaskInfo writes in to %d batches", len(tasks), len(batches))
-        elif checked:
-            if not batches:
-                batches.append({})
+        with self._status_lock:
+            checked = [(name, st) for name, st in statuses if self._check_status(name, st)]
+            if len(batches) <= 1 and checked:
+                if not batches:
+                    batches.append({})
+                for name, st in checked:
+                    batches[0][self._task_status_path(name)] = st.SerializeToString()
+                checked = []
+            for b in batches:
+                try:
+                    self.persister.set_many(b)
+                except PersisterException as e:
+                    raise StateStoreException(e.reason, f"Failed to store {len(b)} TaskInfos") from e
             for name, st in checked:
-                batches[0][self._task_status_path(name)] = st.SerializeToString()
-            checked = []
-        for b in batches:
-            try:
-                self.persister.set_many(b)
-            except PersisterException as e:
-                raise StateStoreException(e.reason, f"Failed to store {len(b)} TaskInfos") from e
-        for name, st in checked:
-            self.store_status(name, st)
+                self.store_status(name, st)
 
     def _check_status(self, task_name: str, status: P.TaskStatus, current=_UNSET) -> bool:
         """The checks ``store_status`` applies before writing (raises on a rejected status);
@@ -193,7 +195,6 @@ class StateStore:
                                       f"Dropping TaskStatus with unknown TaskID: {status.task_id.value}")
         return True
 
-    @_status_write
     def store_status(self, task_name: str, status: P.TaskStatus,
                      properties: Optional[Dict[str, bytes]] = None) -> None:
         """Stores ``status`` (StateStore.storeStatus). ``properties`` are written in the same
@@ -202,7 +203,6 @@ class StateStore:
         warns (DefaultScheduler.java:541-560, StateStoreUtils.storeTaskStatusAsProperty), so a
         property that fails validation is dropped with a warning, and a combined write that fails
         is retried as the status alone."""
-        self._check_status(task_name, status)
         data = status.SerializeToString()
         valid: Dict[str, bytes] = {}
         for k, v in (properties or {}).items():
@@ -213,17 +213,19 @@ class StateStore:
                 self.logger.warning("Not storing property '%s' with the status of %s: %s", k, task_name, e)
                 continue
             valid[self._property_path(k)] = v
-        try:
-            if valid:
-                try:
-                    self.persister.set_many(dict(valid, **{self._task_status_path(task_name): data}))
-                    return
-                except PersisterException as e:
-                    self.logger.warning("Failed to store properties %s with the status of %s (%s); "
-                                        "storing the status alone", sorted(valid), task_name, e)
-            self.persister.set(self._task_status_path(task_name), data)
-        except PersisterException as e:
-            raise StateStoreException(e.reason, str(e)) from e
+        with self._status_lock:
+            self._check_status(task_name, status)
+            try:
+                if valid:
+                    try:
+                        self.persister.set_many(dict(valid, **{self._task_status_path(task_name): data}))
+                        return
+                    except PersisterException as e:
+                        self.logger.warning("Failed to store properties %s with the status of %s (%s); "
+                                            "storing the status alone", sorted(valid), task_name, e)
+                self.persister.set(self._task_status_path(task_name), data)
+            except PersisterException as e:
+                raise StateStoreException(e.reason, str(e)) from e
 
     @_status_write
     def store_statuses(self, items) -> List[Optional[StateStoreException]]:
