@@ -11,6 +11,7 @@ services asking to be uninstalled, unexpected-reservation GC for permanently fai
 decommissioning tasks, region-rule injection and deploy/update plan selection.
 """
 import dataclasses
+import threading
 import textwrap
 import types
 import uuid
@@ -730,3 +731,49 @@ def test_status_batch_falls_back_to_one_write_each(env):
     assert hh.persister.writes - w0 == 1 + 3
     states, _ = _stored(hh.persister)
     assert set(states.values()) == {P.TASK_RUNNING}
+
+
+# ---------------------------------------------------------------------------------------
+# Launch records written behind the evaluation (scheduler.launch_pipeline)
+
+
+def _pipelined(drv, persister):
+    hh = Harness.__new__(Harness)
+    hh.drv, hh.persister = drv, persister
+    FrameworkStore(persister).store_framework_id(U.FRAMEWORK_ID)
+    cfg = SchedulerConfig.for_testing(SDK_PIPELINE_LAUNCH_WRITES="true")
+    s = SchedulerBuilder(service_spec(POD_A, POD_B), cfg, persister).build()
+    s.registered(False)
+    hh.scheduler = s
+    return hh
+
+
+def test_pipelined_launch_is_recorded_before_it_is_sent(env):
+    persister = _CountingPersister()
+    hh = _pipelined(env, persister)
+    sent = []
+
+    def stream(recs):
+        # the ACCEPT goes out only once the TaskInfo is durable
+        launch = launched_task(recs)
+        assert StateStore(persister).fetch_task(launch.name) is not None
+        sent.append(op_types(recs))
+    hh.scheduler.get_client_status()
+    resp = hh.scheduler.offers([offer_for_a()], launch_stream=stream)
+    assert resp.streamed and sent == [FULL_LAUNCH]
+    assert op_types(resp.recommendations) == FULL_LAUNCH
+    assert not any(t.name == "launch-writer" for t in threading.enumerate())
+
+
+def test_pipelined_launch_whose_record_fails_is_dropped(env):
+    persister = _CountingPersister()
+    hh = _pipelined(env, persister)
+    sent = []
+    hh.scheduler.get_client_status()
+
+    def failing_set_many(path_bytes):
+        from dcos_commons_amd.storage.persister import PersisterException, Reason
+        raise PersisterException(Reason.STORAGE_ERROR, "injected")
+    persister.set_many = failing_set_many
+    resp = hh.scheduler.offers([offer_for_a()], launch_stream=sent.append)
+    assert sent == [] and resp.recommendations == []   # the offer is left unused (declined by the cycle)
