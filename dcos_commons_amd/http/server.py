@@ -62,8 +62,11 @@ class _Handler(BaseHTTPRequestHandler):
         self.send_header("Content-Type", resp.content_type)
         self.send_header("Content-Length", str(len(payload)))
         # status line, headers and body in one write (BaseHTTPRequestHandler.end_headers would
-        # flush the headers on their own)
-        self._headers_buffer.append(b"\r\n")
+        # flush the headers on their own; an HTTP/0.9 request gets no header buffer at all)
+        if not hasattr(self, "_headers_buffer"):
+            self._headers_buffer = []
+        else:
+            self._headers_buffer.append(b"\r\n")
         if method != "HEAD":
             self._headers_buffer.append(payload)
         self.flush_headers()

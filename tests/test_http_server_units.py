@@ -84,3 +84,30 @@ def test_scheduler_runner_stop_is_bounded():
     finally:
         SchedulerRunner.stop = orig
     assert stops and max(stops) < 0.05, stops
+
+
+def test_keep_alive_requests_are_not_held_back_by_delayed_acks():
+    """Each response leaves in one write with TCP_NODELAY: a client polling over one keep-alive
+    connection used to stall ~40 ms per request (headers sent, body held by Nagle until the
+    client's delayed ACK)."""
+    import http.client
+
+    from dcos_commons_amd.http.server import ApiServer
+    from dcos_commons_amd.scheduler.scheduler_config import SchedulerConfig
+
+    started = threading.Event()
+    srv = ApiServer.start(SchedulerConfig.for_testing(PORT_API="0"), [], started.set, port=0)
+    assert started.wait(5)
+    conn = http.client.HTTPConnection("127.0.0.1", srv.port, timeout=5)
+    try:
+        conn.request("GET", "/v1/metrics")
+        conn.getresponse().read()
+        t0 = time.perf_counter()
+        for _ in range(20):
+            conn.request("GET", "/v1/metrics")
+            r = conn.getresponse()
+            assert r.status == 200 and r.read()
+        assert time.perf_counter() - t0 < 0.4     # 20 x 40 ms = 0.8 s with the stall
+    finally:
+        conn.close()
+        srv.stop()
