@@ -258,13 +258,18 @@ class _Handler(BaseHTTPRequestHandler):
     def log_message(self, fmt, *args):  # route through logging
         LOGGER.debug("%s " + fmt, self.address_string(), *args)
 
+    def setup(self):
+        super().setup()
+        # events go out as they happen, one small write each: without TCP_NODELAY an event
+        # written while the previous one is unacknowledged waits for the scheduler's delayed ACK
+        self.connection.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+
     def _reply(self, status: int, body: bytes = b"", ctype: str = "text/plain") -> None:
         self.send_response(status)
         self.send_header("Content-Type", ctype)
         self.send_header("Content-Length", str(len(body)))
-        self.end_headers()
-        if body:
-            self.wfile.write(body)
+        self._headers_buffer.append(b"\r\n" + body)   # status line, headers and body in one write
+        self.flush_headers()
 
     def do_GET(self):  # noqa: N802
         if self.path in ("/health", "/master/health"):

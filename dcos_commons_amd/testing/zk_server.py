@@ -442,6 +442,12 @@ class _Conn:
     def __init__(self, server: ZkServer, sock: socket.socket):
         self.server = server
         self.sock = sock
+        # as ZooKeeper's server does (NIOServerCnxnFactory: tcpNoDelay): replies to pipelined
+        # requests and watch events go out back to back, not behind the client's delayed ACK
+        try:
+            sock.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+        except OSError:
+            pass
         self.session: Optional[_Session] = None
         self.send_lock = threading.Lock()
         self.closed = False
