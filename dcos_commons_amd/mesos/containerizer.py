@@ -22,12 +22,19 @@ makes each agent behave like a Mesos agent with the Mesos containerizer and the 
   changes are reported on ``TASK_RUNNING`` updates and ``consecutive_failures`` failures past the
   grace period kill the task (``TASK_KILLED``, ``healthy=false``).
 
+Process start-up and reaping go through ``sdk-agent-launcher`` (``native/agent/launcher.cpp``) when
+it is built: the sandbox is prepared here, the native helper forks, execs and reaps outside the
+interpreter, and reports starts and exits back over a socket (``SDK_NATIVE_AGENT_LAUNCHER=0``, or no
+binary: ``subprocess.Popen`` plus a waiter thread per task, as before). Task processes, readiness
+checks and health checks all start that way.
+
 Test hooks: ``exec_in_task`` (``dcos task exec``), ``kill_with_pattern`` (``pkill -9 -f`` limited
 to the sessions this runtime started) and ``sandbox_of``. Every process this runtime starts is in a
 session it owns; ``shutdown()`` kills them all.
 """
 from __future__ import annotations
 
+import json
 import logging
 import os
 import re
@@ -116,6 +123,166 @@ def secret_accessible(secret_path: str, space: str) -> bool:
     return own[:len(parent)] == parent
 
 
+class _RemoteProcess:
+    """What the containerizer needs of a ``Popen`` for a process the native launcher started:
+    its pid (a session and process-group leader) and its exit status."""
+
+    def __init__(self, pid: int):
+        self.pid = pid
+        self.returncode: Optional[int] = None
+        self._done = threading.Event()
+
+    def _exited(self, rc: int) -> None:
+        self.returncode = rc
+        self._done.set()
+
+    def wait(self, timeout: Optional[float] = None) -> Optional[int]:
+        self._done.wait(timeout)
+        return self.returncode
+
+    def poll(self) -> Optional[int]:
+        return self.returncode
+
+
+class NativeLauncher:
+    """Client of ``sdk-agent-launcher``: one helper process per containerizer, one socket, one
+    reader thread that turns the helper's events into callbacks. ``launch`` waits only for the
+    fork (the pid); ``run`` (a check command) returns its exit code."""
+
+    def __init__(self, binary: str):
+        import socket
+        import subprocess as sp
+
+        self._ours, theirs = socket.socketpair()
+        self.proc = sp.Popen([binary, "--fd", str(theirs.fileno())], pass_fds=(theirs.fileno(),),
+                             stdin=sp.DEVNULL, close_fds=True)
+        theirs.close()
+        self._send_lock = threading.Lock()
+        self._lock = threading.Lock()
+        self._seq = 0
+        self._waiting: Dict[str, "Future"] = {}            # request id -> started pid / run rc
+        self._procs: Dict[str, tuple] = {}                  # launch id -> (_RemoteProcess, on_exit)
+        self._closed = False
+        self._reader = threading.Thread(target=self._read_loop, name="agent-launcher-events", daemon=True)
+        self._reader.start()
+
+    def _next_id(self) -> str:
+        with self._lock:
+            self._seq += 1
+            return str(self._seq)
+
+    def _request(self, msg: dict) -> "Future":
+        from concurrent.futures import Future
+
+        fut: Future = Future()
+        with self._lock:
+            if self._closed:
+                raise OSError("agent launcher is closed")
+            self._waiting[msg["id"]] = fut
+        line = (json.dumps(msg, separators=(",", ":")) + "\n").encode("utf-8")
+        with self._send_lock:
+            self._ours.sendall(line)
+        return fut
+
+    def launch(self, argv: List[str], exe: str, cwd: str, env: Dict[str, str], stdout: str, stderr: str,
+               on_exit: Callable[["_RemoteProcess", int], None]) -> "_RemoteProcess":
+        """Starts the process; returns once the helper has forked it. ``on_exit(process, rc)``
+        runs on the event thread when it is reaped (possibly before this returns)."""
+        rid = self._next_id()
+        proc = _RemoteProcess(0)
+        with self._lock:
+            self._procs[rid] = (proc, on_exit)
+        try:
+            self._request({"op": "launch", "id": rid, "argv": argv, "exe": exe, "cwd": cwd, "env": env,
+                           "stdout": stdout, "stderr": stderr}).result(30)
+        except BaseException:
+            with self._lock:
+                self._procs.pop(rid, None)
+            raise
+        return proc
+
+    def run(self, argv: List[str], cwd: str, env: Dict[str, str], timeout_s: float) -> int:
+        rid = self._next_id()
+        fut = self._request({"op": "run", "id": rid, "argv": argv, "cwd": cwd, "env": env,
+                             "timeout_ms": int(timeout_s * 1000) if timeout_s and timeout_s > 0 else 0})
+        return int(fut.result())
+
+    def _read_loop(self) -> None:
+        buf = b""
+        try:
+            while True:
+                data = self._ours.recv(65536)
+                if not data:
+                    break
+                buf += data
+                while b"\n" in buf:
+                    line, buf = buf.split(b"\n", 1)
+                    if line:
+                        self._event(json.loads(line))
+        except OSError:
+            pass
+        with self._lock:
+            self._closed = True
+            waiting, self._waiting = self._waiting, {}
+        for fut in waiting.values():
+            if not fut.done():
+                fut.set_exception(OSError("agent launcher exited"))
+
+    def _event(self, ev: dict) -> None:
+        kind, rid = ev.get("ev"), str(ev.get("id", ""))
+        if kind == "exited":
+            with self._lock:
+                entry = self._procs.pop(rid, None)
+            if entry is not None:
+                proc, cb = entry
+                proc._exited(int(ev["rc"]))
+                try:
+                    cb(proc, int(ev["rc"]))
+                except Exception:  # noqa: BLE001
+                    LOGGER.exception("exit callback failed")
+            return
+        with self._lock:
+            fut = self._waiting.pop(rid, None)
+            entry = self._procs.get(rid)
+        if kind == "started" and entry is not None:
+            entry[0].pid = int(ev["pid"])      # set before any exit of it is dispatched (same thread)
+        if fut is None:
+            if kind == "error":
+                LOGGER.error("agent launcher: %s", ev.get("msg"))
+            return
+        if kind == "started":
+            fut.set_result(int(ev["pid"]))
+        elif kind == "ran":
+            fut.set_result(int(ev["rc"]))
+        else:
+            with self._lock:
+                self._procs.pop(rid, None)
+            fut.set_exception(OSError(ev.get("msg") or "launch failed"))
+
+    def close(self) -> None:
+        with self._lock:
+            self._closed = True
+        try:
+            self._ours.sendall(b'{"op":"stop"}\n')
+        except OSError:
+            pass
+        try:
+            self.proc.wait(2)
+        except Exception:  # noqa: BLE001
+            self.proc.kill()
+        self._ours.close()
+
+
+def native_launcher_binary() -> Optional[str]:
+    """The built helper, unless ``SDK_NATIVE_AGENT_LAUNCHER=0``."""
+    if os.environ.get("SDK_NATIVE_AGENT_LAUNCHER", "1").lower() in ("0", "false", "no"):
+        return None
+    from dcos_commons_amd.ops.build import BUILD
+
+    path = os.path.join(BUILD, "sdk-agent-launcher")
+    return path if os.access(path, os.X_OK) else None
+
+
 class ProcessTaskBehavior(TaskBehavior):
     executes_commands = True
 
@@ -137,6 +304,7 @@ class ProcessTaskBehavior(TaskBehavior):
         self.extra_env = dict(extra_env or {})
         self._procs: Dict[str, _Proc] = {}
         self._lock = threading.Lock()
+        self._native = None      # NativeLauncher once started; False: start processes in-process
 
     # -- paths -----------------------------------------------------------------------
     def _agent_dir(self, host: str) -> str:
@@ -170,24 +338,47 @@ class ProcessTaskBehavior(TaskBehavior):
             self._link_container_volumes(sandbox, info, space)
             self._fetch(sandbox, info.command.uris)
             proc.env = self._environment(master, task, agent, sandbox, space)
-            with open(os.path.join(sandbox, "stdout"), "ab") as out, open(os.path.join(sandbox, "stderr"), "ab") as err:
-                # the task's shell is named like the executor that would run it on Mesos, so a
-                # `pkill -f mesos-default-executor` takes the task down with "its executor"
-                # (the trailing `exit $?` keeps that shell alive as the command's parent: bash
-                # would otherwise exec the last command of the list in its place)
-                proc.popen = subprocess.Popen([EXECUTOR_ARGV0, "-c", (info.command.value or "true") + "\nexit $?"],
-                                              executable="/bin/bash", cwd=sandbox, env=proc.env,
-                                              stdin=subprocess.DEVNULL, stdout=out, stderr=err,
-                                              start_new_session=True)
+            # the task's shell is named like the executor that would run it on Mesos, so a
+            # `pkill -f mesos-default-executor` takes the task down with "its executor" (the
+            # trailing `exit $?` keeps that shell alive as the command's parent: bash would
+            # otherwise exec the last command of the list in its place)
+            argv = [EXECUTOR_ARGV0, "-c", (info.command.value or "true") + "\nexit $?"]
+            epoch = task.epoch
+            native = self._native_launcher()
+            if native is not None:
+                proc.popen = native.launch(
+                    argv, "/bin/bash", sandbox, proc.env, os.path.join(sandbox, "stdout"),
+                    os.path.join(sandbox, "stderr"),
+                    on_exit=lambda rp, rc: self._exited(master, task, epoch, proc, rc, rp))
+            else:
+                with open(os.path.join(sandbox, "stdout"), "ab") as out, \
+                        open(os.path.join(sandbox, "stderr"), "ab") as err:
+                    proc.popen = subprocess.Popen(argv, executable="/bin/bash", cwd=sandbox, env=proc.env,
+                                                  stdin=subprocess.DEVNULL, stdout=out, stderr=err,
+                                                  start_new_session=True)
         except Exception as e:  # noqa: BLE001
             LOGGER.exception("failed to start %s", info.name)
             master._schedule(0, master._container_failed, task, task.epoch, str(e))
             proc.exited.set()
             return
-        epoch = task.epoch
-        threading.Thread(target=self._wait, args=(master, task, epoch, proc), name=f"wait-{info.name}",
-                         daemon=True).start()
+        if native is None:
+            threading.Thread(target=self._wait, args=(master, task, epoch, proc), name=f"wait-{info.name}",
+                             daemon=True).start()
         master._schedule(0, master._lifecycle_starting, task, epoch, self.timing(info))
+
+    def _native_launcher(self) -> Optional[NativeLauncher]:
+        if self._native is False:
+            return None
+        if self._native is None:
+            with self._lock:
+                if self._native is None:
+                    binary = native_launcher_binary()
+                    try:
+                        self._native = NativeLauncher(binary) if binary else False
+                    except OSError as e:
+                        LOGGER.warning("native agent launcher unavailable (%s): starting tasks in-process", e)
+                        self._native = False
+        return self._native or None
 
     @staticmethod
     def _dcos_space(master, task, agent) -> Optional[str]:
@@ -320,6 +511,20 @@ class ProcessTaskBehavior(TaskBehavior):
         proc.exited.set()
         master._schedule(0, master._process_exited, task, epoch, rc, proc.killed, proc.unhealthy)
 
+    def _exited(self, master, task, epoch: int, proc: _Proc, rc: int, remote) -> None:
+        """A process the native launcher started was reaped (on the launcher's event thread)."""
+        if proc.popen is None:
+            proc.popen = remote
+        proc.rc = rc
+        proc.health_stop.set()
+        # stragglers of the task: its process group now, the rest of its session off this thread
+        # (a /proc scan costs milliseconds on a busy host and would hold up every other event)
+        self._signal_group(proc, signal.SIGKILL)
+        proc.exited.set()
+        master._schedule(0, master._process_exited, task, epoch, rc, proc.killed, proc.unhealthy)
+        threading.Thread(target=self._signal_session, args=(proc, signal.SIGKILL), name=f"reap-{proc.name}",
+                         daemon=True).start()
+
     def started(self, master, task, epoch: int) -> None:
         """Called when the task reports RUNNING: start its health checks."""
         hc = task.info.health_check if task.info.HasField("health_check") else None
@@ -355,6 +560,12 @@ class ProcessTaskBehavior(TaskBehavior):
                 return
 
     def _run_command(self, proc: _Proc, cmd: str, timeout_s: float) -> int:
+        native = self._native_launcher()
+        if native is not None:
+            try:
+                return native.run(["bash", "-c", cmd], proc.sandbox, proc.env, timeout_s)
+            except OSError:
+                return 127
         try:
             r = subprocess.run(["bash", "-c", cmd], cwd=proc.sandbox, env=proc.env, stdin=subprocess.DEVNULL,
                                stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL,
@@ -496,3 +707,6 @@ class ProcessTaskBehavior(TaskBehavior):
                 self._signal_session(p, signal.SIGKILL)
         for p in procs:
             p.exited.wait(5.0)
+        native, self._native = self._native, False
+        if native:
+            native.close()

@@ -6,6 +6,8 @@
   per-device probe contexts resident; ``amd-gpu-ready``, a CMake target, is its client);
 * ``native/build/sdk-bootstrap``, ``native/build/sdk-cli`` -- C++ task bootstrap and service CLI.
 * ``native/build/keytab-fix`` -- hdfs keytab rewriter run by Kerberized hdfs tasks (HADOOP-16283).
+* ``native/build/sdk-agent-launcher`` -- starts and reaps the local DC/OS stand-in's task processes
+  and check commands outside the master's interpreter (``mesos/containerizer.py``).
 
 Everything is compiled directly with ``hipcc --offload-arch=gfx950`` / ``g++`` (no hipify, no
 JIT cache outside the tree) so the built files travel with the repository snapshot.
@@ -86,7 +88,8 @@ def build_cpp_tools(force: bool = False, verbose: bool = False, sanitize: bool =
         return []
     out = BUILD_SANITIZE if sanitize else BUILD
     os.makedirs(out, exist_ok=True)
-    names = ("sdk-bootstrap", "sdk-cli", "native-tests", "tls-tests", "amd-gpu-ready", "keytab-fix") + (
+    names = ("sdk-bootstrap", "sdk-cli", "native-tests", "tls-tests", "amd-gpu-ready", "keytab-fix",
+             "sdk-agent-launcher") + (
         () if sanitize else ("libsdktls.so",))
     targets = [os.path.join(out, n) for n in names]
     srcs = []
