@@ -143,7 +143,7 @@ class DefaultConfigurationUpdater:
         to_update: List[P.TaskInfo] = []
         needed = {target_id}
         memo: dict = {}
-        for info in self.state_store.fetch_tasks():
+        for info in self.state_store.fetch_tasks_shared():     # updated on copies
             try:
                 cid = TaskLabelReader(info).get_target_configuration()
             except (TaskException, ValueError):

@@ -19,16 +19,27 @@ class TaskEnvRouter:
         self._env = {k: v for k, v in sorted(env.items()) if k.startswith(TASKCFG_PREFIX)}
         self._global: Dict[str, str] = {}
         self._pods: Dict[str, Dict[str, str]] = {}
+        # routed config per pod type: a reference package routes ~300 TASKCFG_ variables and each
+        # spec build asks once per pod type and task
+        self._memo: Dict[str, Dict[str, str]] = {}
 
     def set_all_pods_env(self, key: str, value: str) -> "TaskEnvRouter":
         self._global[key] = value
+        self._memo.clear()
         return self
 
     def set_pod_env(self, pod_type: str, key: str, value: str) -> "TaskEnvRouter":
         self._pods.setdefault(pod_type.lower(), {})[key] = value
+        self._memo.clear()
         return self
 
     def get_config(self, pod_type: str) -> Dict[str, str]:
+        hit = self._memo.get(pod_type)
+        if hit is None:
+            hit = self._memo[pod_type] = self._route(pod_type)
+        return dict(hit)
+
+    def _route(self, pod_type: str) -> Dict[str, str]:
         out = dict(sorted(self._global.items()))
         out.update(self._pods.get(pod_type.lower(), {}))
         pod_prefix = TASKCFG_PREFIX + to_env_name(pod_type) + "_"

@@ -76,7 +76,7 @@ def get_pods_to_decommission(service_spec, tasks) -> List[Tuple[Tuple, List[P.Ta
 
 class DecommissionPlanFactory:
     def __init__(self, service_spec, state_store, namespace: Optional[str] = None):
-        all_tasks = state_store.fetch_tasks()
+        all_tasks = state_store.fetch_tasks_shared()
         self.pods_to_decommission = get_pods_to_decommission(service_spec, all_tasks)
         to_decom = {t.name for _, ts in self.pods_to_decommission for t in ts}
         for t in all_tasks:

@@ -147,7 +147,7 @@ class DefaultScheduler(AbstractScheduler):
         decom = self._decommission_manager()
         if decom is not None:
             active |= {t.name for t in decom.tasks_to_decommission}
-        unneeded = [t for t in self.state_store.fetch_tasks() if t.name not in active]
+        unneeded = [t for t in self.state_store.fetch_tasks_shared() if t.name not in active]
         if self.scheduler_config.use_legacy_unneeded_task_kills():
             for t in unneeded:
                 c = P.TaskInfo()
@@ -271,8 +271,7 @@ class DefaultScheduler(AbstractScheduler):
             for name, data in names.items():
                 hit = cache.get(name)
                 if hit is None or hit[0] != data:
-                    t = P.TaskInfo()
-                    t.ParseFromString(data)
+                    t = self.state_store.shared_task(name, data)
                     hit = cache[name] = (data, frozenset(get_resource_ids(get_all_resources(t))),
                                          is_permanently_failed(t))
                 _, ids, failed = hit

@@ -82,7 +82,7 @@ class PlanScheduler:
             if t.resource_set.id not in sets:
                 continue
             name = f"{pi.name}-{t.name}"
-            info = self.state_store.fetch_task(name)
+            info = self.state_store.fetch_task_shared(name)
             if info is None or not info.task_id.value:
                 continue  # never launched (a footprint placeholder): nothing runs to kill
             status = self.state_store.fetch_status(name)

@@ -223,7 +223,7 @@ class DefaultRecoveryPlanManager(PlanManager):
         out = []
         for failed in self._new_failed_pods(dirty_assets):
             pi = failed.pod_instance
-            infos = [self.state_store.fetch_task(f"{pi.name}-{t}") for t in failed.tasks_to_launch]
+            infos = [self.state_store.fetch_task_shared(f"{pi.name}-{t}") for t in failed.tasks_to_launch]
             infos = [i for i in infos if i is not None]
             rtype = self._task_recovery_type(infos)
             if rtype == RecoveryType.NONE:

@@ -90,7 +90,7 @@ class PersistentLaunchRecorder:
     def _stored_resource_ids(self, pi: PodInstance) -> set:
         out = set()
         for t in pi.pod.tasks:
-            stored = self.state_store.fetch_task(f"{pi.name}-{t.name}")
+            stored = self.state_store.fetch_task_shared(f"{pi.name}-{t.name}")
             if stored is not None:
                 out.update(get_resource_ids(get_all_resources(stored)))
         return out
@@ -118,14 +118,15 @@ class PersistentLaunchRecorder:
             peer = working.get(name)
             if peer is None:
                 if name not in fetched:
-                    fetched[name] = self.state_store.fetch_task(name)
+                    fetched[name] = self.state_store.fetch_task_shared(name)
                 stored = fetched[name]
                 if stored is None:
                     continue
                 if list(stored.resources) == list(info.resources) and (
                         not has_executor or list(stored.executor.resources) == list(info.executor.resources)):
                     continue  # already what this launch would write
-                peer = stored
+                peer = P.TaskInfo()      # the stored one is shared with the state store's readers
+                peer.CopyFrom(stored)
             del peer.resources[:]
             peer.resources.extend(info.resources)
             if has_executor:

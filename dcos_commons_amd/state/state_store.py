@@ -326,25 +326,11 @@ class StateStore:
         set (the test suite sets it) every call first checks that no cached TaskInfo was
         modified since it was handed out."""
         cache = self._shared
-        out = []
         raw = self.fetch_tasks_bytes()
-        for name, data in raw.items():
-            hit = cache.get(name)
-            if hit is not None and (hit[0] is data or hit[0] == data):
-                if _DEBUG_SHARED and hit[1].SerializeToString() != hit[0]:
-                    raise AssertionError(f"a caller modified the shared TaskInfo of {name}")
-                out.append(hit[1])
-                continue
-            t = P.TaskInfo()
-            try:
-                t.ParseFromString(data)
-            except Exception as e:  # noqa: BLE001
-                raise StateStoreException(Reason.SERIALIZATION_ERROR, str(e)) from e
-            cache[name] = (data, t)
-            out.append(t)
+        out = [self.shared_task(name, data) for name, data in raw.items()]
         if len(cache) > len(raw):
             for gone in set(cache) - set(raw):
-                del cache[gone]
+                cache.pop(gone, None)       # another reader may have dropped it first
         return out
 
     def fetch_task_shared(self, task_name: str) -> Optional[P.TaskInfo]:
@@ -352,8 +338,12 @@ class StateStore:
         plans built at a scheduler start read the same tasks once per plan that has a step for
         them). Callers must not modify the returned TaskInfo."""
         data = self.fetch_task_bytes(task_name)
-        if data is None:
-            return None
+        return None if data is None else self.shared_task(task_name, data)
+
+    def shared_task(self, task_name: str, data: bytes) -> P.TaskInfo:
+        """The shared parsed TaskInfo of ``task_name`` for its stored bytes ``data`` (as read by
+        ``fetch_task_bytes`` / ``fetch_tasks_bytes``): parsed once per distinct bytes, whichever
+        reader asks first. Callers must not modify it."""
         hit = self._shared.get(task_name)
         if hit is not None and (hit[0] is data or hit[0] == data):
             if _DEBUG_SHARED and hit[1].SerializeToString() != hit[0]:

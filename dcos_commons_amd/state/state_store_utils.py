@@ -41,7 +41,7 @@ def fetch_task_info(store: StateStore, status: P.TaskStatus) -> P.TaskInfo:
         name = common_id_utils.to_task_name(status.task_id)
     except Exception as e:  # noqa: BLE001
         raise StateStoreException(Reason.SERIALIZATION_ERROR, str(e)) from e
-    info = store.fetch_task(name)
+    info = store.fetch_task_shared(name)     # callers read it (and copy before any change)
     if info is None:
         raise StateStoreException(Reason.NOT_FOUND, f"Failed to find a task with TaskID: {status.task_id.value}")
     return info
@@ -54,7 +54,7 @@ def repair_task_ids(store: StateStore) -> None:
 
     repaired_statuses = {}
     repaired_tasks = []
-    for task in store.fetch_tasks():
+    for task in store.fetch_tasks_shared():     # repairs are made on copies
         status = store.fetch_status(task.name)
         if status is not None:
             if task.task_id.value == "" and is_terminal(status):

@@ -483,6 +483,8 @@ class OverrideStore:
     def fetch_tasks(self):
         return list(TASKS)
 
+    fetch_tasks_shared = fetch_tasks
+
     def fetch_goal_override_status(self, name):
         return self.overrides[name]
 
