@@ -128,13 +128,26 @@ class _RemoteProcess:
     its pid (a session and process-group leader) and its exit status."""
 
     def __init__(self, pid: int):
-        self.pid = pid
+        self.pid = pid                  # 0 until the helper reports the fork (an unwaited launch)
         self.returncode: Optional[int] = None
         self._done = threading.Event()
+        self._started = threading.Event()
+        if pid:
+            self._started.set()
+
+    def _set_pid(self, pid: int) -> None:
+        self.pid = pid
+        self._started.set()
 
     def _exited(self, rc: int) -> None:
         self.returncode = rc
+        self._started.set()
         self._done.set()
+
+    def wait_started(self, timeout: Optional[float] = None) -> int:
+        """The pid once the helper has forked the process (0: it never started)."""
+        self._started.wait(timeout)
+        return self.pid
 
     def wait(self, timeout: Optional[float] = None) -> Optional[int]:
         self._done.wait(timeout)
@@ -161,7 +174,7 @@ class NativeLauncher:
         self._lock = threading.Lock()
         self._seq = 0
         self._waiting: Dict[str, "Future"] = {}            # request id -> started pid / run rc
-        self._procs: Dict[str, tuple] = {}                  # launch id -> (_RemoteProcess, on_exit)
+        self._procs: Dict[str, tuple] = {}      # launch id -> (_RemoteProcess, on_exit, on_error, on_started)
         self._closed = False
         self._reader = threading.Thread(target=self._read_loop, name="agent-launcher-events", daemon=True)
         self._reader.start()
@@ -185,21 +198,42 @@ class NativeLauncher:
         return fut
 
     def launch(self, argv: List[str], exe: str, cwd: str, env: Dict[str, str], stdout: str, stderr: str,
-               on_exit: Callable[["_RemoteProcess", int], None]) -> "_RemoteProcess":
-        """Starts the process; returns once the helper has forked it. ``on_exit(process, rc)``
-        runs on the event thread when it is reaped (possibly before this returns)."""
+               on_exit: Callable[["_RemoteProcess", int], None], setup: Optional[List[tuple]] = None,
+               on_error: Optional[Callable[["_RemoteProcess", str], None]] = None,
+               on_started: Optional[Callable[["_RemoteProcess"], None]] = None) -> "_RemoteProcess":
+        """Starts the process after the helper has run the sandbox ``setup``, in order:
+        ``("d", dir)`` creates a directory with its parents, ``("l", target, link)`` symlinks
+        ``link`` to ``target`` unless it exists. ``on_exit(process, rc)`` runs on the event thread when it is
+        reaped. Without ``on_error`` this returns once the helper has forked it (a failure raises
+        ``OSError``); with it, it returns at once: the pid is filled in when the fork is reported
+        (``wait_started``) and ``on_started(process)`` runs on the event thread, or a failed set-up
+        or fork calls ``on_error(process, message)`` there instead."""
         rid = self._next_id()
         proc = _RemoteProcess(0)
         with self._lock:
-            self._procs[rid] = (proc, on_exit)
+            self._procs[rid] = (proc, on_exit, on_error, on_started)
+        msg = {"op": "launch", "id": rid, "argv": argv, "exe": exe, "cwd": cwd, "env": env,
+               "stdout": stdout, "stderr": stderr}
+        if setup:
+            msg["setup"] = [list(step) for step in setup]
         try:
-            self._request({"op": "launch", "id": rid, "argv": argv, "exe": exe, "cwd": cwd, "env": env,
-                           "stdout": stdout, "stderr": stderr}).result(30)
+            if on_error is not None:
+                self._send(msg)
+            else:
+                self._request(msg).result(30)
         except BaseException:
             with self._lock:
                 self._procs.pop(rid, None)
             raise
         return proc
+
+    def _send(self, msg: dict) -> None:
+        with self._lock:
+            if self._closed:
+                raise OSError("agent launcher is closed")
+        line = (json.dumps(msg, separators=(",", ":")) + "\n").encode("utf-8")
+        with self._send_lock:
+            self._ours.sendall(line)
 
     def run(self, argv: List[str], cwd: str, env: Dict[str, str], timeout_s: float) -> int:
         rid = self._next_id()
@@ -224,9 +258,18 @@ class NativeLauncher:
         with self._lock:
             self._closed = True
             waiting, self._waiting = self._waiting, {}
+            unstarted = [(rid, e) for rid, e in self._procs.items() if not e[0].pid and e[2] is not None]
+            for rid, _ in unstarted:
+                self._procs.pop(rid, None)
         for fut in waiting.values():
             if not fut.done():
                 fut.set_exception(OSError("agent launcher exited"))
+        for _, (proc, _, on_error, _) in unstarted:
+            proc._exited(127)
+            try:
+                on_error(proc, "agent launcher exited")
+            except Exception:  # noqa: BLE001
+                LOGGER.exception("launch error callback failed")
 
     def _event(self, ev: dict) -> None:
         kind, rid = ev.get("ev"), str(ev.get("id", ""))
@@ -234,7 +277,7 @@ class NativeLauncher:
             with self._lock:
                 entry = self._procs.pop(rid, None)
             if entry is not None:
-                proc, cb = entry
+                proc, cb = entry[0], entry[1]
                 proc._exited(int(ev["rc"]))
                 try:
                     cb(proc, int(ev["rc"]))
@@ -245,10 +288,24 @@ class NativeLauncher:
             fut = self._waiting.pop(rid, None)
             entry = self._procs.get(rid)
         if kind == "started" and entry is not None:
-            entry[0].pid = int(ev["pid"])      # set before any exit of it is dispatched (same thread)
+            entry[0]._set_pid(int(ev["pid"]))   # set before any exit of it is dispatched (same thread)
+            if entry[3] is not None:
+                try:
+                    entry[3](entry[0])
+                except Exception:  # noqa: BLE001
+                    LOGGER.exception("launch started callback failed")
         if fut is None:
             if kind == "error":
-                LOGGER.error("agent launcher: %s", ev.get("msg"))
+                if entry is not None and entry[2] is not None:
+                    with self._lock:
+                        self._procs.pop(rid, None)
+                    entry[0]._exited(127)
+                    try:
+                        entry[2](entry[0], str(ev.get("msg") or "launch failed"))
+                    except Exception:  # noqa: BLE001
+                        LOGGER.exception("launch error callback failed")
+                else:
+                    LOGGER.error("agent launcher: %s", ev.get("msg"))
             return
         if kind == "started":
             fut.set_result(int(ev["pid"]))
@@ -328,28 +385,38 @@ class ProcessTaskBehavior(TaskBehavior):
         eid = task.executor_id or "command"
         sandbox = os.path.join(self._agent_dir(host), "frameworks", _safe(task.framework_id), "executors",
                                _safe(eid), "tasks", _safe(info.task_id.value))
-        os.makedirs(sandbox, exist_ok=True)
+        native = self._native_launcher()
+        resources = list(info.resources) + self._executor_resources(master, task, agent)
+        # with the native helper, the sandbox and its volume links are made by the helper, off the
+        # master's thread (secrets and fetched URIs still need this process: done here first)
+        plan = self._sandbox_plan(host, sandbox, resources, info) if native is not None else None
         proc = _Proc(info.task_id.value, info.name, host, sandbox, {})
         with self._lock:
             self._procs[proc.task_id] = proc
+        epoch = task.epoch
         try:
             space = self._dcos_space(master, task, agent)
-            self._link_volumes(host, sandbox, list(info.resources) + self._executor_resources(master, task, agent))
-            self._link_container_volumes(sandbox, info, space)
-            self._fetch(sandbox, info.command.uris)
+            if plan is None:
+                os.makedirs(sandbox, exist_ok=True)
+                self._link_volumes(host, sandbox, resources)
+                self._link_container_volumes(sandbox, info, space)
+                self._fetch(sandbox, info.command.uris)
             proc.env = self._environment(master, task, agent, sandbox, space)
             # the task's shell is named like the executor that would run it on Mesos, so a
             # `pkill -f mesos-default-executor` takes the task down with "its executor" (the
             # trailing `exit $?` keeps that shell alive as the command's parent: bash would
             # otherwise exec the last command of the list in its place)
             argv = [EXECUTOR_ARGV0, "-c", (info.command.value or "true") + "\nexit $?"]
-            epoch = task.epoch
-            native = self._native_launcher()
             if native is not None:
                 proc.popen = native.launch(
                     argv, "/bin/bash", sandbox, proc.env, os.path.join(sandbox, "stdout"),
                     os.path.join(sandbox, "stderr"),
-                    on_exit=lambda rp, rc: self._exited(master, task, epoch, proc, rc, rp))
+                    on_exit=lambda rp, rc: self._exited(master, task, epoch, proc, rc, rp),
+                    setup=plan,
+                    on_error=lambda rp, msg: self._launch_failed(master, task, epoch, proc, msg),
+                    # STARTING / RUNNING once the process exists, as an executor reports them
+                    on_started=lambda rp: master._schedule(0, master._lifecycle_starting, task, epoch,
+                                                           self.timing(info)))
             else:
                 with open(os.path.join(sandbox, "stdout"), "ab") as out, \
                         open(os.path.join(sandbox, "stderr"), "ab") as err:
@@ -364,7 +431,47 @@ class ProcessTaskBehavior(TaskBehavior):
         if native is None:
             threading.Thread(target=self._wait, args=(master, task, epoch, proc), name=f"wait-{info.name}",
                              daemon=True).start()
-        master._schedule(0, master._lifecycle_starting, task, epoch, self.timing(info))
+            master._schedule(0, master._lifecycle_starting, task, epoch, self.timing(info))
+
+    def _sandbox_plan(self, host: str, sandbox: str, resources: List[P.Resource], info: P.TaskInfo):
+        """The sandbox set-up steps for the native helper, in the order ``_link_volumes`` and
+        ``_link_container_volumes`` take them: the sandbox, each persistent volume's directory and
+        its link at the container path, then host / sandbox path volumes. None when the task also
+        needs a secret file or fetched URIs written into its sandbox."""
+        if info.command.uris:
+            return None
+        steps: list = [("d", sandbox)]
+
+        def link(target: str, container_path: str) -> None:
+            if container_path and not os.path.isabs(container_path):   # absolute: needs a mount namespace
+                steps.append(("l", target, os.path.join(sandbox, container_path)))
+        for r in resources:
+            if not r.HasField("disk") or not r.disk.HasField("persistence") or not r.disk.persistence.id:
+                continue
+            if r.disk.HasField("source") and r.disk.source.type == P.Resource.DiskInfo.Source.MOUNT:
+                target = os.path.join(self.mount_dir(host, r.disk.source.mount.root), _safe(r.disk.persistence.id))
+            else:
+                target = self.volume_dir(host, r.disk.persistence.id)
+            steps.append(("d", target))
+            link(target, r.disk.volume.container_path)
+        for v in info.container.volumes:
+            src = v.source
+            if src.type == P.Volume.Source.SECRET:
+                return None
+            if src.type == P.Volume.Source.HOST_PATH or v.host_path:
+                link(src.host_path.path or v.host_path, v.container_path)
+            elif src.type == P.Volume.Source.SANDBOX_PATH:
+                target = os.path.join(sandbox, src.sandbox_path.path)
+                steps.append(("d", target))
+                link(target, v.container_path)
+        return steps
+
+    def _launch_failed(self, master, task, epoch: int, proc: _Proc, msg: str) -> None:
+        """The helper could not set up the sandbox or fork (on the launcher's event thread)."""
+        LOGGER.error("failed to start %s: %s", proc.name, msg)
+        proc.health_stop.set()
+        proc.exited.set()
+        master._schedule(0, master._container_failed, task, epoch, msg)
 
     def _native_launcher(self) -> Optional[NativeLauncher]:
         if self._native is False:
@@ -598,11 +705,23 @@ class ProcessTaskBehavior(TaskBehavior):
         self._terminate(proc, grace)
         return True
 
+    @staticmethod
+    def _pid(proc: _Proc) -> int:
+        """The task's session leader; 0 when it never started. A launch handed to the native
+        helper without waiting may not have reported its fork yet: wait for it (briefly)."""
+        p = proc.popen
+        if p is None:
+            return 0
+        if not p.pid and isinstance(p, _RemoteProcess):
+            return p.wait_started(5.0)
+        return p.pid
+
     def _signal_session(self, proc: _Proc, sig: int) -> int:
-        if proc.popen is None:
+        sid = self._pid(proc)
+        if sid <= 0:
             return 0
         n = 0
-        for pid in _session_pids(proc.popen.pid):
+        for pid in _session_pids(sid):
             try:
                 os.kill(pid, sig)
                 n += 1
@@ -614,10 +733,11 @@ class ProcessTaskBehavior(TaskBehavior):
     def _signal_group(proc: _Proc, sig: int) -> None:
         """The task's process group (its session leader's group: ``bash -c`` and whatever it runs
         without job control), in one ``killpg`` instead of a ``/proc`` scan."""
-        if proc.popen is None:
+        pgid = ProcessTaskBehavior._pid(proc)
+        if pgid <= 0:       # never started (killpg(0) would signal this process's own group)
             return
         try:
-            os.killpg(proc.popen.pid, sig)
+            os.killpg(pgid, sig)
         except (ProcessLookupError, PermissionError):
             pass
 
@@ -677,9 +797,10 @@ class ProcessTaskBehavior(TaskBehavior):
                      and (agent_host is None or p.agent_host == agent_host)]
         matches = []
         for p in procs:
-            if p.popen is None:
+            sid = self._pid(p)
+            if sid <= 0:
                 continue
-            for pid in _session_pids(p.popen.pid):
+            for pid in _session_pids(sid):
                 if rx.search(_cmdline(pid)):
                     matches.append(pid)
         if oldest and matches:

@@ -13,8 +13,12 @@
 //   sdk-agent-launcher --fd N      (N: a connected stream socket, e.g. one end of a socketpair)
 //
 // Requests and events are newline-delimited JSON objects:
-//   {"op":"launch","id":I,"argv":[...],"exe":PATH,"cwd":DIR,"env":{...},"stdout":F,"stderr":F}
+//   {"op":"launch","id":I,"argv":[...],"exe":PATH,"cwd":DIR,"env":{...},"stdout":F,"stderr":F,
+//    "setup":[["d",DIR] | ["l",TARGET,LINK] ...]}
 //        -> {"ev":"started","id":I,"pid":P} | {"ev":"error","id":I,"msg":M};  later {"ev":"exited","id":I,"rc":R}
+//        The sandbox set-up comes first, in the helper, in order: "d" creates DIR with its parents
+//        (an existing one is fine); "l" makes LINK (parents created) a symlink to TARGET unless
+//        LINK exists already. A failure there is an "error".
 //   {"op":"run","id":I,"argv":[...],"cwd":DIR,"env":{...},"timeout_ms":T}
 //        -> {"ev":"ran","id":I,"rc":R}   (stdio on /dev/null; R = 124 when killed at the timeout)
 //   {"op":"stop"}                         -> the helper exits (it never kills: the caller owns that)
@@ -26,6 +30,7 @@
 #include <signal.h>
 #include <sys/signalfd.h>
 #include <sys/socket.h>
+#include <sys/stat.h>
 #include <sys/wait.h>
 #include <fcntl.h>
 #include <unistd.h>
@@ -82,6 +87,47 @@ std::vector<std::string> strings(const Json& a) {
   if (a.is_array())
     for (const auto& v : a.arr()) out.push_back(v.as_text());
   return out;
+}
+
+// mkdir -p: every missing component of `path`, mode 0755. False (errno set) on a real failure.
+bool make_dirs(const std::string& path) {
+  if (path.empty()) return true;
+  struct stat st;
+  if (::stat(path.c_str(), &st) == 0) {
+    if (S_ISDIR(st.st_mode)) return true;
+    errno = ENOTDIR;
+    return false;
+  }
+  size_t slash = path.find_last_of('/');
+  if (slash != std::string::npos && slash > 0 && !make_dirs(path.substr(0, slash))) return false;
+  if (::mkdir(path.c_str(), 0755) == 0 || errno == EEXIST) return true;
+  return false;
+}
+
+// The sandbox set-up of a launch request; an empty string when it all succeeded, else what failed.
+std::string prepare(const Json& req) {
+  const Json& steps = req["setup"];
+  if (!steps.is_array()) return "";
+  for (const auto& st : steps.arr()) {
+    if (!st.is_array() || st.arr().empty()) return "bad set-up entry";
+    const auto& a = st.arr();
+    const std::string kind = a[0].as_text();
+    if (kind == "d" && a.size() == 2) {
+      if (!make_dirs(a[1].as_text())) return "mkdir " + a[1].as_text() + ": " + std::strerror(errno);
+    } else if (kind == "l" && a.size() == 3) {
+      const std::string target = a[1].as_text(), link = a[2].as_text();
+      size_t slash = link.find_last_of('/');
+      if (slash != std::string::npos && slash > 0 && !make_dirs(link.substr(0, slash)))
+        return "mkdir " + link.substr(0, slash) + ": " + std::strerror(errno);
+      struct stat sb;
+      if (::lstat(link.c_str(), &sb) == 0) continue;   // already there (a relaunch in place)
+      if (::symlink(target.c_str(), link.c_str()) != 0 && errno != EEXIST)
+        return "symlink " + link + ": " + std::strerror(errno);
+    } else {
+      return "bad set-up entry " + kind;
+    }
+  }
+  return "";
 }
 
 // fork + exec in a new session; stdio from the given files (empty: /dev/null). Returns the pid,
@@ -142,6 +188,15 @@ void handle(const Json& req) {
     e.set("msg", "empty argv");
     send_event(e);
     return;
+  }
+  if (!run) {
+    std::string failed = prepare(req);
+    if (!failed.empty()) {
+      Json e = event("error", id);
+      e.set("msg", failed);
+      send_event(e);
+      return;
+    }
   }
   pid_t pid = spawn(req["exe"].is_null() ? "" : req["exe"].as_text(), argv, req["cwd"].is_null() ? "" : req["cwd"].as_text(),
                     req["env"], run ? "" : req["stdout"].as_text(), run ? "" : req["stderr"].as_text());

@@ -101,3 +101,47 @@ def test_helper_exits_when_its_client_goes_away(binary):
     nl = NativeLauncher(binary)
     nl._ours.shutdown(socket.SHUT_RDWR)    # the master process died: its end of the socket is gone
     assert nl.proc.wait(5) == 0
+
+
+def test_unwaited_launch_sets_up_the_sandbox_first(launcher, tmp_path):
+    """The containerizer's launch: the helper creates the sandbox and the volume directories,
+    links the volumes at their container paths, then forks; the caller does not wait for the pid."""
+    sandbox = tmp_path / "agent" / "frameworks" / "fw" / "tasks" / "t1"
+    volume = tmp_path / "agent" / "volumes" / "v1"
+    (tmp_path / "existing").mkdir()
+    exits, errors, done = [], [], threading.Event()
+
+    def on_exit(proc, rc):
+        exits.append(rc)
+        done.set()
+    p = launcher.launch(["mesos-default-executor", "-c", "ls data/ >/dev/null && echo ok > data/f\nexit $?"], "/bin/bash",
+                        str(sandbox), ENV, str(sandbox / "stdout"), str(sandbox / "stderr"), on_exit,
+                        setup=[("d", str(sandbox)), ("d", str(volume)), ("l", str(volume), str(sandbox / "data")),
+                               ("l", str(tmp_path / "existing"), str(sandbox / "a" / "b")),
+                               ("d", str(sandbox / "data"))],     # in order: the link is there first
+                        on_error=lambda proc, msg: errors.append(msg))
+    assert p.wait_started(10) > 0
+    assert done.wait(10) and exits == [0] and errors == []
+    assert (volume / "f").read_text() == "ok\n"
+    assert os.path.islink(sandbox / "data") and os.readlink(sandbox / "a" / "b") == str(tmp_path / "existing")
+    # a relaunch in place: the links exist already and are kept
+    done.clear()
+    launcher.launch(["x", "-c", "cat data/f"], "/bin/bash", str(sandbox), ENV, str(sandbox / "stdout2"), "",
+                    on_exit, setup=[("d", str(sandbox)), ("l", str(volume), str(sandbox / "data"))],
+                    on_error=lambda proc, msg: errors.append(msg))
+    assert done.wait(10) and errors == [] and (sandbox / "stdout2").read_text() == "ok\n"
+
+
+def test_unwaited_launch_reports_a_failed_set_up(launcher, tmp_path):
+    blocker = tmp_path / "file"
+    blocker.write_text("not a directory")
+    failed, done = [], threading.Event()
+
+    def on_error(proc, msg):
+        failed.append((proc.pid, msg))
+        done.set()
+    p = launcher.launch(["x", "-c", "true"], "/bin/bash", str(blocker / "sandbox"), ENV, "", "",
+                        lambda proc, rc: None, setup=[("d", str(blocker / "sandbox"))], on_error=on_error)
+    assert done.wait(10)
+    assert failed[0][0] == 0 and "mkdir" in failed[0][1]
+    assert p.wait_started(1) == 0 and p.poll() == 127
