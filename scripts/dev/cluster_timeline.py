@@ -19,6 +19,7 @@ from dcos_commons_amd.mesos.local_master import LocalMaster
 pods = int(sys.argv[1]) if len(sys.argv) > 1 else 8
 cycles = int(sys.argv[2]) if len(sys.argv) > 2 else 2
 logging.basicConfig(level=logging.ERROR)
+sys.setswitchinterval(CB.CLUSTER_SWITCH_INTERVAL_MS / 1000.0)    # as cluster_bench runs
 events = []
 lock = threading.Lock()
 
