@@ -253,7 +253,7 @@ class DefaultRecoveryPlanManager(PlanManager):
                 if hit is not None and hit[0] == ib and hit[1] == sb:
                     hit = (ib, sb) + hit[2:]
                 else:
-                    info = P.TaskInfo.FromString(ib)
+                    info = self.state_store.shared_task(name, ib)     # read-only here
                     status = P.TaskStatus.FromString(sb) if sb is not None else None
                     need = (status is not None and
                             bool(task_utils.get_tasks_needing_recovery(self.config_store, [info], [status])))
