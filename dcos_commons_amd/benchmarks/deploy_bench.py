@@ -154,7 +154,7 @@ class DeployBench:
 
     @staticmethod
     def _pod_ready(state_store, task_name: str, old_task_id: Optional[str]) -> bool:
-        info = state_store.fetch_task(task_name)
+        info = state_store.fetch_task_shared(task_name)    # the observer only reads it
         st = state_store.fetch_status(task_name)
         if info is None or st is None or st.state != P.TASK_RUNNING:
             return False
