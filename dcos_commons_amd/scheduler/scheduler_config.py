@@ -266,7 +266,7 @@ class SchedulerConfig:
         handled; unpinned, that took an 8-agent deploy from 58 to 41 ms on a slow CPU, but with the
         process pinned to a few cores (bench.py) it only added tail latency (8-pod deploys with
         22-37 ms outliers against <= 16 ms at 5 ms, profiles/ab_gil_interval_pinned_r03.txt)."""
-        return self.env.get_optional_int("SDK_GIL_SWITCH_INTERVAL_MS", 0) / 1000.0
+        return float(self.env.get_optional("SDK_GIL_SWITCH_INTERVAL_MS", "0") or 0) / 1000.0
 
     def gc_gen0_threshold(self) -> int:
         """Allocations between young-generation collections of the cyclic garbage collector
