@@ -23,10 +23,13 @@ makes each agent behave like a Mesos agent with the Mesos containerizer and the 
   grace period kill the task (``TASK_KILLED``, ``healthy=false``).
 
 Process start-up and reaping go through ``sdk-agent-launcher`` (``native/agent/launcher.cpp``) when
-it is built: the sandbox is prepared here, the native helper forks, execs and reaps outside the
-interpreter, and reports starts and exits back over a socket (``SDK_NATIVE_AGENT_LAUNCHER=0``, or no
-binary: ``subprocess.Popen`` plus a waiter thread per task, as before). Task processes, readiness
-checks and health checks all start that way.
+it is built: the helper creates the sandbox and links its volumes (an ordered list of set-up steps
+in the launch request; a task with secret files or URIs to fetch has its sandbox prepared here
+first), forks, execs and reaps outside the interpreter, and reports starts and exits back over a
+socket. The master does not wait for the fork: STARTING is reported when the helper reports the
+process started, as an executor reports it (``SDK_NATIVE_AGENT_LAUNCHER=0``, or no binary:
+``subprocess.Popen`` plus a waiter thread per task, as before). Task processes, readiness checks
+and health checks all start that way.
 
 Test hooks: ``exec_in_task`` (``dcos task exec``), ``kill_with_pattern`` (``pkill -9 -f`` limited
 to the sessions this runtime started) and ``sandbox_of``. Every process this runtime starts is in a
@@ -159,8 +162,9 @@ class _RemoteProcess:
 
 class NativeLauncher:
     """Client of ``sdk-agent-launcher``: one helper process per containerizer, one socket, one
-    reader thread that turns the helper's events into callbacks. ``launch`` waits only for the
-    fork (the pid); ``run`` (a check command) returns its exit code."""
+    reader thread that turns the helper's events into callbacks. ``launch`` waits at most for the
+    fork (the pid), or not at all when given ``on_error``; ``run`` (a check command) returns its
+    exit code."""
 
     def __init__(self, binary: str):
         import socket
