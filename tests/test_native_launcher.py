@@ -7,7 +7,10 @@ to the sandbox files; the environment and working directory are exactly the ones
 process leads its own session (so the containerizer can signal the whole task); a signalled
 process reports ``-signal`` as ``subprocess`` does; ``run`` returns a command's exit code, 124 at
 its timeout (the process group is killed) and 127 when the program does not exist; the helper
-exits when its client goes away. Runs against the release and the ASan/UBSan builds.
+exits when its client goes away. An unwaited launch runs its sandbox set-up (directories, volume
+links, in order) in the helper, and a failed set-up is reported instead of a start; through the
+containerizer, STARTING is scheduled on the helper's started event and a sandbox the helper cannot
+create fails the container. Runs against the release and the ASan/UBSan builds.
 """
 import os
 import signal
@@ -145,3 +148,89 @@ def test_unwaited_launch_reports_a_failed_set_up(launcher, tmp_path):
     assert done.wait(10)
     assert failed[0][0] == 0 and "mkdir" in failed[0][1]
     assert p.wait_started(1) == 0 and p.poll() == 127
+
+
+class _FakeMaster:
+    """What ProcessTaskBehavior.launch needs of LocalMaster: ``_schedule`` and the callbacks it names."""
+
+    def __init__(self):
+        self.calls = []
+        self.event = threading.Event()
+
+    def _schedule(self, delay, fn, *args):
+        self.calls.append((fn.__name__, args))
+        self.event.set()
+
+    def _lifecycle_starting(self, *a):
+        pass
+
+    def _container_failed(self, *a):
+        pass
+
+    def _process_exited(self, *a):
+        pass
+
+    def wait_for(self, name, timeout=10):
+        deadline = time.time() + timeout
+        while time.time() < deadline:
+            hit = [args for fn, args in self.calls if fn == name]
+            if hit:
+                return hit[0]
+            self.event.wait(0.05)
+            self.event.clear()
+        raise AssertionError(f"{name} not scheduled: {self.calls}")
+
+
+def _task_and_agent(cmd, volume_path="data"):
+    from types import SimpleNamespace
+
+    from dcos_commons_amd.mesos import protos as P
+
+    info = P.TaskInfo(name="hello-0-server")
+    info.task_id.value = "svc__hello-0-server__1"
+    info.command.value = cmd
+    r = info.resources.add(name="disk", type=P.Value.SCALAR)
+    r.scalar.value = 10
+    r.disk.persistence.id = "vol-1"
+    r.disk.volume.container_path = volume_path
+    task = SimpleNamespace(info=info, framework_id="fw", executor_id="", epoch=1, gpu_devices=[])
+    agent = SimpleNamespace(spec=SimpleNamespace(hostname="10.0.0.1"), id="agent-1", executors={})
+    return task, agent
+
+
+def test_containerizer_launches_through_the_helper_and_reports_start_then_exit(binary, tmp_path, monkeypatch):
+    from dcos_commons_amd.mesos import containerizer as C
+
+    monkeypatch.setattr(C, "native_launcher_binary", lambda: binary)
+    beh = C.ProcessTaskBehavior(str(tmp_path / "work"))
+    master = _FakeMaster()
+    task, agent = _task_and_agent("echo hi > data/out")
+    try:
+        beh.launch(master, task, agent)
+        master.wait_for("_lifecycle_starting")          # reported once the helper has forked
+        args = master.wait_for("_process_exited")
+        assert args[2] == 0                             # rc
+        sandbox = beh.sandbox_of(task.info.task_id.value)
+        assert os.path.islink(os.path.join(sandbox, "data"))
+        assert open(os.path.join(beh.volume_dir("10.0.0.1", "vol-1"), "out")).read() == "hi\n"
+    finally:
+        beh.shutdown()
+
+
+def test_containerizer_reports_a_sandbox_the_helper_cannot_create(binary, tmp_path, monkeypatch):
+    from dcos_commons_amd.mesos import containerizer as C
+
+    monkeypatch.setattr(C, "native_launcher_binary", lambda: binary)
+    beh = C.ProcessTaskBehavior(str(tmp_path / "work"))
+    (tmp_path / "work" / "10.0.0.1").write_text("a file where the agent directory should be")
+    master = _FakeMaster()
+    task, agent = _task_and_agent("true")
+    try:
+        beh.launch(master, task, agent)
+        args = master.wait_for("_container_failed")
+        assert "mkdir" in args[2]
+        assert not [fn for fn, _ in master.calls if fn == "_lifecycle_starting"]
+        # a kill of the task that never started signals nothing (no process group 0)
+        assert beh.kill(master, task) is False
+    finally:
+        beh.shutdown()
