@@ -106,6 +106,16 @@ def _start_ticks(pid: int) -> int:
         return 1 << 62
 
 
+def _alive(pid: int) -> bool:
+    """The process exists and is not a zombie (an orphan whose new parent has not reaped it)."""
+    try:
+        with open(f"/proc/{pid}/stat", "rb") as f:
+            stat = f.read().decode("utf-8", "replace")
+        return stat[stat.rindex(")") + 2:].split()[0] != "Z"
+    except (OSError, ValueError, IndexError):
+        return False
+
+
 def _cmdline(pid: int) -> str:
     try:
         with open(f"/proc/{pid}/cmdline", "rb") as f:
@@ -180,6 +190,7 @@ class NativeLauncher:
         self._waiting: Dict[str, "Future"] = {}            # request id -> started pid / run rc
         self._procs: Dict[str, tuple] = {}      # launch id -> (_RemoteProcess, on_exit, on_error, on_started)
         self._closed = False
+        self._stopping = False
         self._reader = threading.Thread(target=self._read_loop, name="agent-launcher-events", daemon=True)
         self._reader.start()
 
@@ -265,6 +276,13 @@ class NativeLauncher:
             unstarted = [(rid, e) for rid, e in self._procs.items() if not e[0].pid and e[2] is not None]
             for rid, _ in unstarted:
                 self._procs.pop(rid, None)
+            orphans, self._procs = list(self._procs.values()), {}
+        if orphans and not self._stopping:
+            # the helper died under running processes: they live on (reparented), but their exit
+            # status is gone with it. Watch for their end and report it as a kill.
+            LOGGER.warning("agent launcher exited with %d processes running: watching them", len(orphans))
+            threading.Thread(target=self._watch_orphans, args=(orphans,), name="agent-launcher-orphans",
+                             daemon=True).start()
         for fut in waiting.values():
             if not fut.done():
                 fut.set_exception(OSError("agent launcher exited"))
@@ -320,7 +338,31 @@ class NativeLauncher:
                 self._procs.pop(rid, None)
             fut.set_exception(OSError(ev.get("msg") or "launch failed"))
 
+    @staticmethod
+    def _watch_orphans(orphans) -> None:
+        live = [(proc, cb) for proc, cb, _, _ in orphans if proc.pid > 0]
+        while live:
+            still = []
+            for proc, cb in live:
+                if _alive(proc.pid):
+                    still.append((proc, cb))
+                    continue
+                proc._exited(-signal.SIGKILL)
+                try:
+                    cb(proc, -signal.SIGKILL)
+                except Exception:  # noqa: BLE001
+                    LOGGER.exception("exit callback failed")
+            live = still
+            if live:
+                time.sleep(0.05)
+
+    @property
+    def closed(self) -> bool:
+        """The helper is gone (it exited, or ``close`` was called)."""
+        return self._closed
+
     def close(self) -> None:
+        self._stopping = True
         with self._lock:
             self._closed = True
         try:
@@ -480,8 +522,11 @@ class ProcessTaskBehavior(TaskBehavior):
     def _native_launcher(self) -> Optional[NativeLauncher]:
         if self._native is False:
             return None
-        if self._native is None:
+        if self._native is None or self._native.closed:
             with self._lock:
+                if self._native is not None and self._native is not False and self._native.closed:
+                    LOGGER.warning("native agent launcher exited: starting a new one")
+                    self._native = None
                 if self._native is None:
                     binary = native_launcher_binary()
                     try:

@@ -234,3 +234,32 @@ def test_containerizer_reports_a_sandbox_the_helper_cannot_create(binary, tmp_pa
         assert beh.kill(master, task) is False
     finally:
         beh.shutdown()
+
+
+def test_a_dead_helper_is_replaced_and_its_running_processes_are_watched(binary, tmp_path, monkeypatch):
+    from dcos_commons_amd.mesos import containerizer as C
+
+    monkeypatch.setattr(C, "native_launcher_binary", lambda: binary)
+    beh = C.ProcessTaskBehavior(str(tmp_path / "work"))
+    try:
+        first = beh._native_launcher()
+        exits, done = [], threading.Event()
+
+        def on_exit(proc, rc):
+            exits.append(rc)
+            done.set()
+        p = first.launch(["x", "-c", "sleep 0.3"], "/bin/bash", str(tmp_path), ENV, "", "", on_exit,
+                         on_error=lambda proc, msg: None)
+        assert p.wait_started(10) > 0
+        first.proc.kill()                        # the helper dies under a running process
+        first.proc.wait(5)
+        assert done.wait(10)                     # its end is still reported (as a kill: the status is lost)
+        assert exits == [-signal.SIGKILL]
+        deadline = time.time() + 5
+        while not first.closed and time.time() < deadline:
+            time.sleep(0.01)
+        second = beh._native_launcher()          # the next launch gets a new helper
+        assert second is not first and not second.closed
+        assert second.run(["bash", "-c", "exit 5"], str(tmp_path), ENV, 5) == 5
+    finally:
+        beh.shutdown()
