@@ -35,8 +35,7 @@ import socket
 import threading
 import time
 import urllib.parse
-import zlib
-from typing import Dict, Iterable, List, Optional
+from typing import Iterable, List, Optional
 
 from dcos_commons_amd.framework.driver import SchedulerDriver
 from dcos_commons_amd.mesos import protos as P
@@ -77,7 +76,7 @@ class V1HttpSchedulerDriver(SchedulerDriver):
                  implicit_acknowledgements: bool = True, reconnect: bool = False,
                  heartbeat_misses: int = 5, connect_timeout_s: float = 10.0,
                  backoff_s: float = 0.5, max_backoff_s: float = 10.0, token_provider=None,
-                 async_calls: bool = False, call_lanes: int = 1):
+                 async_calls: bool = False):
         if content_type not in (PROTOBUF, JSON):
             raise ValueError(f"unsupported content type {content_type}")
         self.master_url = master_url.rstrip("/")
@@ -112,19 +111,10 @@ class V1HttpSchedulerDriver(SchedulerDriver):
         # logged, not raised). The offer thread then does not wait for an ACCEPT's HTTP round trip,
         # nor the event stream for an ACKNOWLEDGE's before it reads the next event.
         self.async_calls = async_calls
-        # call_lanes > 1 (async only): calls that name an agent (ACCEPT / DECLINE through their
-        # offers' agent, ACKNOWLEDGE, KILL with an agent, MESSAGE) go out on the lane of that agent,
-        # each lane its own sender thread and keep-alive connection, so the ACCEPTs of one offer
-        # cycle for eight agents are not eight sequential round trips. Calls for one agent keep
-        # their order; calls naming no agent go on lane 0.
-        self.call_lanes = max(1, int(call_lanes)) if async_calls else 1
-        self._lanes: List["collections.deque[P.Call]"] = [collections.deque() for _ in range(self.call_lanes)]
-        self._outbox = self._lanes[0]
+        self._outbox: "collections.deque[P.Call]" = collections.deque()
         self._outbox_cond = threading.Condition()
         self._in_flight = 0
         self._sender: Optional[threading.Thread] = None
-        self._senders: List[Optional[threading.Thread]] = [None] * self.call_lanes
-        self._offer_agents: Dict[str, str] = {}     # offer id -> agent id, for routing ACCEPT / DECLINE
 
     # -- lifecycle ---------------------------------------------------------------------
     @property
@@ -257,58 +247,25 @@ class V1HttpSchedulerDriver(SchedulerDriver):
                 self._conns.append(conn)
         return conn
 
-    def _lane(self, call: P.Call) -> int:
-        if self.call_lanes == 1:
-            return 0
-        agent = ""
-        t = call.type
-        if t == P.Call.ACCEPT or t == P.Call.DECLINE:
-            ids = call.accept.offer_ids if t == P.Call.ACCEPT else call.decline.offer_ids
-            with self._outbox_cond:
-                for oid in ids:
-                    agent = self._offer_agents.pop(oid.value, "") or agent
-        elif t == P.Call.ACKNOWLEDGE:
-            agent = call.acknowledge.agent_id.value
-        elif t == P.Call.KILL and call.kill.HasField("agent_id"):
-            agent = call.kill.agent_id.value
-        elif t == P.Call.MESSAGE:
-            agent = call.message.agent_id.value
-        return zlib.crc32(agent.encode("utf-8")) % self.call_lanes if agent else 0
-
-    def _note_offers(self, offers) -> None:
-        if self.call_lanes == 1:
-            return
-        with self._outbox_cond:
-            if len(self._offer_agents) > 10000:      # offers that were rescinded or expired unseen
-                self._offer_agents.clear()
-            for o in offers:
-                self._offer_agents[o.id.value] = o.agent_id.value
-
     def _send(self, call: P.Call) -> None:
         if not self.async_calls:
             self._send_now(call)
             return
-        lane = self._lane(call)
         with self._outbox_cond:
-            self._lanes[lane].append(call)
-            if self._senders[lane] is None:
-                th = threading.Thread(target=self._send_loop, args=(lane,),
-                                      name="mesos-v1-calls" + (f"-{lane}" if lane else ""), daemon=True)
-                self._senders[lane] = th
-                if lane == 0:
-                    self._sender = th
-                th.start()
-            self._outbox_cond.notify_all()
+            self._outbox.append(call)
+            if self._sender is None:
+                self._sender = threading.Thread(target=self._send_loop, name="mesos-v1-calls", daemon=True)
+                self._sender.start()
+            self._outbox_cond.notify()
 
-    def _send_loop(self, lane: int = 0) -> None:
-        box = self._lanes[lane]
+    def _send_loop(self) -> None:
         while True:
             with self._outbox_cond:
-                while not box:
+                while not self._outbox:
                     if self._stopped.is_set():
                         return
                     self._outbox_cond.wait(0.5)
-                call = box.popleft()
+                call = self._outbox.popleft()
                 self._in_flight += 1
             try:
                 self._send_now(call)
@@ -325,9 +282,9 @@ class V1HttpSchedulerDriver(SchedulerDriver):
             return True
         deadline = time.monotonic() + timeout_s
         with self._outbox_cond:
-            while any(self._lanes) or self._in_flight:
+            while self._outbox or self._in_flight:
                 left = deadline - time.monotonic()
-                if left <= 0 or not any(th is not None and th.is_alive() for th in self._senders):
+                if left <= 0 or self._sender is None or not self._sender.is_alive():
                     return False
                 self._outbox_cond.wait(min(left, 0.05))
         return True
@@ -526,7 +483,6 @@ class V1HttpSchedulerDriver(SchedulerDriver):
             else:
                 self._call_scheduler("registered", P.FrameworkID(value=self._framework_id), self.master_info)
         elif t == P.Event.OFFERS:
-            self._note_offers(ev.offers.offers)
             self._call_scheduler("resource_offers", list(ev.offers.offers))
         elif t == P.Event.RESCIND:
             self._call_scheduler("offer_rescinded", ev.rescind.offer_id)

@@ -343,12 +343,6 @@ class SchedulerConfig:
         v = self.env.get_optional("SDK_PIPELINE_LAUNCH_WRITES", "")
         return None if v in ("", "auto") else v.lower() in ("1", "true", "yes")
 
-    def mesos_call_lanes(self) -> int:
-        """Sender lanes of the v1 HTTP driver (``SDK_MESOS_CALL_LANES``, default 1): with more, the
-        calls of different agents go out on parallel keep-alive connections (one agent's calls
-        stay in order). No reference counterpart: libprocess sends every call on its own."""
-        return max(1, self.env.get_optional_int("SDK_MESOS_CALL_LANES", 1))
-
     def launch_reconcile_s(self) -> float:
         """Explicitly reconcile a launch that still has no status after this many seconds, e.g.
         because its ACCEPT was lost (0 = reference behaviour: wait for the next scheduler

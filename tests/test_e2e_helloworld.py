@@ -31,8 +31,7 @@ def hello_env(hello=2, world=2):
 
 
 class Cluster:
-    def __init__(self, spec_file="svc.yml", agents=3, gpus=0, env=None, transport="local", driver_kwargs=None,
-                 **cfg):
+    def __init__(self, spec_file="svc.yml", agents=3, gpus=0, env=None, transport="local", **cfg):
         self.env = env or hello_env()
         overrides = {"PORT_API": "0", "SDK_OFFER_WAIT_S": "0.5"}
         overrides.update(cfg)
@@ -52,8 +51,7 @@ class Cluster:
 
             self.http_master = HttpMaster(self.master, heartbeat_s=1.0).start()
             ctype = JSON if transport == "json" else PROTOBUF
-            factory = lambda s, i: V1HttpSchedulerDriver(self.http_master.url, s, i, content_type=ctype,  # noqa: E731
-                                                         **(driver_kwargs or {}))
+            factory = lambda s, i: V1HttpSchedulerDriver(self.http_master.url, s, i, content_type=ctype)  # noqa: E731
         self.runner = SchedulerRunner(SchedulerBuilder(self.spec, self.cfg, self.persister).set_plans_from(raw),
                                       driver_factory=factory)
 

@@ -490,63 +490,3 @@ def test_updates_read_together_reach_the_scheduler_together(cluster):
         assert [n for b in batches for n in b] == names[len(names) - sum(len(b) for b in batches):]
     finally:
         d.stop()
-
-
-def test_call_lanes_keep_each_agents_calls_in_order(monkeypatch):
-    """With several sender lanes, an agent's calls (ACCEPT / DECLINE through the agent of their
-    offers, ACKNOWLEDGE) all go out on that agent's lane in submission order; calls naming no
-    agent go on lane 0; ``flush`` waits for every lane."""
-    d = V1HttpSchedulerDriver("http://127.0.0.1:1", Recorder(), P.FrameworkInfo(name="fw"), async_calls=True,
-                              call_lanes=4)
-    sent = []
-    lock = threading.Lock()
-
-    def fake_send_now(call):
-        time.sleep(0.001)
-        agent = {P.Call.ACKNOWLEDGE: call.acknowledge.agent_id.value}.get(call.type, "")
-        if call.type == P.Call.ACCEPT:
-            agent = call.accept.offer_ids[0].value.split("-")[0]
-        with lock:
-            sent.append((threading.current_thread().name, P.Call.Type.Name(call.type), agent, call))
-    monkeypatch.setattr(d, "_send_now", fake_send_now)
-    offers = []
-    for a in range(8):
-        o = P.Offer(hostname=f"h{a}")
-        o.id.value, o.agent_id.value, o.framework_id.value = f"a{a}-offer", f"a{a}", "fw"
-        offers.append(o)
-    d._note_offers(offers)
-    for o in offers:
-        d.accept_offers([o.id], [])
-        st = P.TaskStatus(uuid=b"u")
-        st.agent_id.CopyFrom(o.agent_id)
-        st.task_id.value = "t"
-        d.acknowledge_status_update(st)
-    d.revive_offers()
-    try:
-        assert d.flush(5.0)
-        assert len(sent) == 17
-        by_agent = {}
-        for thread, kind, agent, _ in sent:
-            if agent:
-                by_agent.setdefault(agent, []).append((thread, kind))
-        for agent, calls in by_agent.items():
-            assert [k for _, k in calls] == ["ACCEPT", "ACKNOWLEDGE"], (agent, calls)
-            assert len({t for t, _ in calls}) == 1      # one lane per agent
-        assert len({t for t, _, a, _ in sent if a}) > 1   # the agents are spread over lanes
-        assert [t for t, k, _, _ in sent if k == "REVIVE"] == ["mesos-v1-calls"]
-        assert d._offer_agents == {}                   # routed offers are forgotten
-    finally:
-        d._stopped.set()
-
-
-def test_helloworld_over_http_with_call_lanes():
-    ProcessExit.set_test_mode(True)
-    with Cluster(transport="protobuf", driver_kwargs={"async_calls": True, "call_lanes": 3}) as c:
-        c.wait_plan("deploy")
-        states = c.master.task_states()
-        assert len(states) == 4 and set(states.values()) == {P.TASK_RUNNING}
-        old = c.store.fetch_task("hello-0-server").task_id.value
-        c.master.fail_task(old)
-        c.wait(lambda: c.store.fetch_status("hello-0-server").task_id.value != old and
-               c.store.fetch_status("hello-0-server").state == P.TASK_RUNNING)
-        c.wait_plan("recovery")
