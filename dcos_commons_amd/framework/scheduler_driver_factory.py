@@ -78,8 +78,7 @@ class SchedulerDriverFactory:
                                          credential=credential, content_type=scheduler_config.mesos_content_type(),
                                          reconnect=scheduler_config.is_driver_reconnect(),
                                          token_provider=token_provider,
-                                         async_calls=scheduler_config.is_async_mesos_calls(),
-                                         update_window_s=scheduler_config.status_update_window_s())
+                                         async_calls=scheduler_config.is_async_mesos_calls())
         from dcos_commons_amd.mesos.local_master import LocalSchedulerDriver, local_master_from_env
 
         return LocalSchedulerDriver(local_master_from_env(scheduler_config.env), scheduler, framework_info)

@@ -31,7 +31,6 @@ import collections
 import http.client
 import json
 import logging
-import select
 import socket
 import threading
 import time
@@ -77,7 +76,7 @@ class V1HttpSchedulerDriver(SchedulerDriver):
                  implicit_acknowledgements: bool = True, reconnect: bool = False,
                  heartbeat_misses: int = 5, connect_timeout_s: float = 10.0,
                  backoff_s: float = 0.5, max_backoff_s: float = 10.0, token_provider=None,
-                 async_calls: bool = False, update_window_s: float = 0.0):
+                 async_calls: bool = False):
         if content_type not in (PROTOBUF, JSON):
             raise ValueError(f"unsupported content type {content_type}")
         self.master_url = master_url.rstrip("/")
@@ -116,9 +115,6 @@ class V1HttpSchedulerDriver(SchedulerDriver):
         self._outbox_cond = threading.Condition()
         self._in_flight = 0
         self._sender: Optional[threading.Thread] = None
-        # update_window_s > 0: UPDATE events that end a read are held this long for more of them
-        # (a task's STARTING and RUNNING arrive microseconds apart), so they are stored together
-        self.update_window_s = max(0.0, float(update_window_s))
 
     # -- lifecycle ---------------------------------------------------------------------
     @property
@@ -414,20 +410,16 @@ class V1HttpSchedulerDriver(SchedulerDriver):
         # has arrived is decoded in one pass (http.client returns one chunk per read)
         chunks = recordio.ChunkedDecoder() if resp.chunked else None
         read = resp.fp.read1 if chunks is not None else resp.read1
-        carried: List[P.TaskStatus] = []     # trailing updates held for the update window
-        window_end = 0.0
         while not self._stopped.is_set():
             try:
                 data = read(65536)
             except socket.timeout:
                 raise OSError("missed heartbeats") from None
             if not data:
-                if carried:
-                    self._on_updates(carried)
                 return
             if chunks is not None:
                 data = chunks.feed(data)
-            updates, carried = carried, []
+            updates: List[P.TaskStatus] = []
             for rec in dec.feed(data):
                 ev = decode_message(P.Event, rec, self.content_type)
                 if ev.type == P.Event.UPDATE:
@@ -440,32 +432,9 @@ class V1HttpSchedulerDriver(SchedulerDriver):
                     updates = []
                 self._on_event(ev)
             if updates:
-                if not window_end:
-                    window_end = time.monotonic() + self.update_window_s
-                if self.update_window_s > 0 and self._more_within(window_end - time.monotonic()):
-                    carried = updates      # more is arriving: read it and deliver them together
-                    continue
                 self._on_updates(updates)
-            window_end = 0.0
             if chunks is not None and chunks.done:
                 return
-
-    def _more_within(self, timeout: float) -> bool:
-        """Whether the event stream has more bytes within ``timeout`` seconds."""
-        if timeout <= 0:
-            return False
-        conn = self._stream_conn
-        sock = getattr(conn, "sock", None) if conn is not None else None
-        if sock is None:
-            return False
-        if getattr(sock, "pending", None) is not None and sock.pending() > 0:     # TLS: decrypted, unread
-            return True
-        try:
-            poller = select.poll()      # (not select(): the stream's descriptor may be past FD_SETSIZE)
-            poller.register(sock.fileno(), select.POLLIN)
-            return bool(poller.poll(timeout * 1000.0))
-        except (OSError, ValueError):
-            return False
 
     def _on_updates(self, statuses: List[P.TaskStatus]) -> None:
         if len(statuses) == 1 or getattr(self.scheduler, "status_updates", None) is None:

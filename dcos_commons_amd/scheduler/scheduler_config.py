@@ -343,12 +343,6 @@ class SchedulerConfig:
         v = self.env.get_optional("SDK_PIPELINE_LAUNCH_WRITES", "")
         return None if v in ("", "auto") else v.lower() in ("1", "true", "yes")
 
-    def status_update_window_s(self) -> float:
-        """How long the v1 driver holds the UPDATE events that end a read of the event stream for
-        more of them, so that statuses arriving together are stored in one write
-        (``SDK_STATUS_UPDATE_WINDOW_US``, default 0: deliver at once). No reference counterpart."""
-        return max(0.0, float(self.env.get_optional("SDK_STATUS_UPDATE_WINDOW_US", "0") or 0)) / 1e6
-
     def launch_reconcile_s(self) -> float:
         """Explicitly reconcile a launch that still has no status after this many seconds, e.g.
         because its ACCEPT was lost (0 = reference behaviour: wait for the next scheduler

@@ -490,47 +490,3 @@ def test_updates_read_together_reach_the_scheduler_together(cluster):
         assert [n for b in batches for n in b] == names[len(names) - sum(len(b) for b in batches):]
     finally:
         d.stop()
-
-
-@pytest.mark.parametrize("window_s,expected", [
-    (0.05, [[P.TASK_STARTING, P.TASK_RUNNING]]),
-    (0.0, [[P.TASK_STARTING], [P.TASK_RUNNING]]),
-])
-def test_update_window_joins_updates_that_arrive_just_apart(cluster, window_s, expected):
-    """With an update window, a status that arrives shortly after another is handed over with it
-    (one ``status_updates`` call, so one write); without it each goes alone."""
-    got = []
-
-    class Batching(Recorder):
-        def status_updates(self, driver, statuses):
-            got.append([s.state for s in statuses])
-
-        def status_update(self, driver, status):
-            got.append([status.state])
-
-    lm, hm = cluster
-    rec = Batching()
-    d = V1HttpSchedulerDriver(hm.url, rec, P.FrameworkInfo(name="fw", role="r"), update_window_s=window_s)
-    d.start()
-    try:
-        rec.wait_for("registered")
-        fid = d.framework_id
-        deadline = time.time() + 5
-        while fid not in hm.subscriptions and time.time() < deadline:
-            time.sleep(0.01)
-        sub = hm.subscriptions[fid]
-
-        def send(state):
-            st = P.TaskStatus(state=state)
-            st.task_id.value = "t1"
-            sub.scheduler.status_update(None, st)
-        send(P.TASK_STARTING)
-        time.sleep(0.005)
-        send(P.TASK_RUNNING)
-        deadline = time.time() + 5
-        while sum(map(len, got)) < 2 and time.time() < deadline:
-            time.sleep(0.01)
-        time.sleep(0.1)
-        assert got == expected
-    finally:
-        d.stop()
