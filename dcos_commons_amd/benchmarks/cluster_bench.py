@@ -220,6 +220,16 @@ class ClusterBench:
 CLUSTER_SWITCH_INTERVAL_MS = 0.5
 
 
+def readiness_label(probe_cmd: str, probe_service: bool) -> str:
+    """What gates a pod's readiness in a row, so a row whose check is a shell ``test`` is never
+    read as a GPU-checked one."""
+    if probe_service:
+        return "GPU readiness: amd-gpu-ready -> node service amd-gpu-probed (HIP MFMA/HBM probe on the pod's GPU)"
+    if "amd-gpu-probe" in probe_cmd:
+        return "GPU readiness: amd-gpu-probe binary per check (HIP runtime started per check)"
+    return "no GPU readiness (the check only tests that HIP_VISIBLE_DEVICES was injected)"
+
+
 def main(argv: Optional[List[str]] = None) -> int:
     from dcos_commons_amd.benchmarks.deploy_bench import PROFILES
 
@@ -272,6 +282,7 @@ def main(argv: Optional[List[str]] = None) -> int:
                       "scheduler_env": dict(kv.split("=", 1) for kv in args.scheduler_env),
                       "cluster_switch_interval_ms": args.cluster_switch_interval_ms or None,
                       "probe_service_checks": served,
+                      "readiness": readiness_label(args.probe_cmd, args.probe_service),
                       "deploy_s": stat("deploy_s"), "mttr_restart_s": stat("mttr_restart_s"),
                       "mttr_replace_s": stat("mttr_replace_s"),
                       "data": "scheduler process + v1 HTTP API + ZooKeeper; helloworld gpu.yml, gpus:1 per pod"}),

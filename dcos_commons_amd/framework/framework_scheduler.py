@@ -244,3 +244,6 @@ class FrameworkScheduler:
     def stop(self) -> None:
         self.offer_processor.stop()
         self.implicit_reconciler.stop()
+        close = getattr(self.client, "close", None)
+        if callable(close):
+            close()

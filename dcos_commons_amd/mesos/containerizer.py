@@ -238,7 +238,12 @@ class NativeLauncher:
                 self._request(msg).result(30)
         except BaseException:
             with self._lock:
-                self._procs.pop(rid, None)
+                pending = self._procs.pop(rid, None)
+            if pending is None and on_error is not None:
+                # the helper died between registering the launch and sending it: the read loop
+                # already popped the entry and reported the failure through on_error, so raising
+                # here would report the same task's failure a second time
+                return proc
             raise
         return proc
 

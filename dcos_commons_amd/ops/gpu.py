@@ -33,12 +33,15 @@ recorded directory (``kfd/``, ``amd_smi_static.json``, ``rocminfo.txt``) instead
 from __future__ import annotations
 
 import json
+import logging
 import os
 import re
 import socket
 import subprocess
 from dataclasses import dataclass, field, replace
-from typing import Dict, Iterable, List, Mapping, Optional, Sequence, Tuple
+from typing import Dict, Iterable, List, Mapping, Optional, Sequence, Tuple, Union
+
+LOGGER = logging.getLogger(__name__)
 
 KFD_TOPOLOGY = "/sys/class/kfd/kfd/topology"
 IOLINK_TYPE_XGMI = 11  # kfd_ioctl.h / kfd_crat.h: CRAT_IOLINK_TYPE_XGMI
@@ -422,30 +425,63 @@ def merge(base: GpuInventory, *refinements: GpuInventory) -> GpuInventory:
     return GpuInventory(devices, "+".join([base.source] + [r.source for r in refinements if r.devices]))
 
 
-def parse_visible_devices(value: Optional[str]) -> Optional[List[int]]:
-    """``HIP_VISIBLE_DEVICES``-style list (``0,2,3``); None when unset or empty (the ROCm
-    runtime only filters on a non-empty value; containers often export the variable empty)."""
+def parse_visible_devices(value: Optional[str]) -> Optional[List[Union[int, str]]]:
+    """``HIP_VISIBLE_DEVICES``-style list (``0,2,3``, or ROCm's ``GPU-<unique id>`` UUIDs, which
+    come back as strings); None when unset or empty (the ROCm runtime only filters on a non-empty
+    value; containers often export the variable empty)."""
     if value is None:
         return None
     value = value.strip()
     if not value:
         return None
-    out = []
+    out: List[Union[int, str]] = []
     for tok in value.split(","):
         tok = tok.strip()
         if tok.isdigit():
             out.append(int(tok))
+        elif tok:
+            out.append(tok)
+    return out
+
+
+def _uuid_key(tok: str) -> str:
+    t = tok.lower()
+    if t.startswith("gpu-"):
+        t = t[4:]
+    return t.lstrip("0") or "0"
+
+
+def _resolve_selection(sel: List[Union[int, str]], devices: List["GpuDevice"]) -> Optional[List[int]]:
+    """Positions in ``devices`` that ``sel`` names: an index, or a UUID matched against the
+    device's KFD ``unique_id``. None when a token names nothing this inventory can identify (the
+    caller then does not filter, rather than silently advertising zero GPUs: ADVICE r5)."""
+    by_uuid = {_uuid_key(d.unique_id): n for n, d in enumerate(devices) if d.unique_id}
+    out = []
+    for tok in sel:
+        if isinstance(tok, int):
+            out.append(tok)
+        elif _uuid_key(tok) in by_uuid:
+            out.append(by_uuid[_uuid_key(tok)])
+        else:
+            return None
     return out
 
 
 def apply_visibility(inv: GpuInventory, env: Mapping[str, str], already_filtered: bool = False) -> GpuInventory:
     """Restrict and renumber as the ROCm runtime does: ``ROCR_VISIBLE_DEVICES`` selects among the
     node's devices, then ``HIP_VISIBLE_DEVICES`` among those; the survivors are numbered 0..n-1
-    (xGMI peers are kept only among the survivors)."""
+    (xGMI peers are kept only among the survivors). UUID entries (``GPU-<unique id>``) select the
+    device with that unique id; a selection with an entry that matches no device is ignored with
+    a warning."""
     devices = list(inv.devices)
     for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES"):
-        sel = parse_visible_devices(env.get(var))
+        raw = parse_visible_devices(env.get(var))
+        if raw is None:
+            continue
+        sel = _resolve_selection(raw, devices)
         if sel is None:
+            LOGGER.warning("%s=%r names a device this node's inventory cannot identify; not filtering on it",
+                           var, env.get(var))
             continue
         if already_filtered and any(i >= len(devices) for i in sel):
             # the tools only saw the devices this container was granted: the selection named

@@ -245,6 +245,11 @@ class DefaultScheduler(AbstractScheduler):
             recs = [r for r in recs if id(r) not in dropped]
         return OfferResponse.processed(recs, streamed=True)
 
+    def close(self) -> None:
+        """Ends the launch writer thread (scheduler shutdown)."""
+        if self._pipeline:
+            self._pipeline.close()
+
     def _launch_pipeline(self):
         if self._pipeline is None:
             on = _cfg_pipeline(self.scheduler_config)

@@ -24,31 +24,38 @@ LOGGER = logging.getLogger(__name__)
 
 
 class LaunchPipeline:
+    """One writer thread per scheduler, started at the first submit and parked on the condition
+    variable between offer cycles (a thread per cycle would also give the v1 driver, in sync-call
+    mode, one new keep-alive master connection per cycle: ADVICE r5)."""
+
     def __init__(self, record: Callable[[list], bool], name: str = "launch-writer"):
         self._record = record          # -> False when the write failed (its operations are dropped)
         self._name = name
         self._cv = threading.Condition()
         self._queue: List[Tuple[list, Callable[[list], None]]] = []
         self._busy = False
-        self._closing = False
+        self._closed = False
         self._failed: List[list] = []
         self._thread: Optional[threading.Thread] = None
         self.writes = 0                # records written (for tests and traces)
+        self.threads_started = 0       # writer threads started over the pipeline's life (tests)
 
     def submit(self, recs: list, send: Callable[[list], None]) -> None:
         """Queue one step's recommendations; ``send(recs)`` ACCEPTs them once recorded."""
         with self._cv:
+            if self._closed:
+                raise RuntimeError("launch pipeline is closed")
             self._queue.append((recs, send))
             if self._thread is None:
-                self._closing = False
                 self._thread = threading.Thread(target=self._run, name=self._name, daemon=True)
+                self.threads_started += 1
                 self._thread.start()
             self._cv.notify_all()
 
     def _run(self) -> None:
         while True:
             with self._cv:
-                while not self._queue and not self._closing:
+                while not self._queue and not self._closed:
                     self._cv.wait()
                 if not self._queue:
                     self._thread = None
@@ -76,12 +83,19 @@ class LaunchPipeline:
                     self._cv.notify_all()
 
     def drain(self) -> List[list]:
-        """Waits until every submitted step is recorded and sent (the writer thread then exits);
-        returns the recommendation lists whose record failed."""
+        """Waits until every submitted step is recorded and sent (the writer then parks until the
+        next cycle submits); returns the recommendation lists whose record failed."""
         with self._cv:
-            self._closing = True
-            self._cv.notify_all()
-            while self._queue or self._busy or self._thread is not None:
+            while self._queue or self._busy:
                 self._cv.wait()
             failed, self._failed = self._failed, []
         return failed
+
+    def close(self, timeout: float = 5.0) -> None:
+        """Finishes what is queued, then ends the writer thread."""
+        with self._cv:
+            self._closed = True
+            self._cv.notify_all()
+            thread = self._thread
+        if thread is not None and thread is not threading.current_thread():
+            thread.join(timeout)

@@ -146,7 +146,11 @@ pid_t spawn(const std::string& exe, const std::vector<std::string>& argv, const 
 
   pid_t pid = ::fork();
   if (pid != 0) return pid;
-  // child: own session (pgid = pid), default signal dispositions, stdio, cwd, exec
+  // child: own session (pgid = pid), default signal dispositions, stdio, cwd, exec. Ignored
+  // signals survive fork and execve, and the helper ignores SIGPIPE (main), so the task gets SIGPIPE
+  // and SIGXFSZ back at their defaults, as subprocess's restore_signals does for the Popen path.
+  ::signal(SIGPIPE, SIG_DFL);
+  ::signal(SIGXFSZ, SIG_DFL);
   sigset_t none;
   sigemptyset(&none);
   ::sigprocmask(SIG_SETMASK, &none, nullptr);

@@ -762,7 +762,11 @@ def test_pipelined_launch_is_recorded_before_it_is_sent(env):
     resp = hh.scheduler.offers([offer_for_a()], launch_stream=stream)
     assert resp.streamed and sent == [FULL_LAUNCH]
     assert op_types(resp.recommendations) == FULL_LAUNCH
-    assert not any(t.name == "launch-writer" for t in threading.enumerate())
+    # one writer thread serves the scheduler's cycles; it ends when the scheduler closes
+    writer = hh.scheduler._pipeline._thread
+    assert writer is not None and writer.is_alive()
+    hh.scheduler.close()
+    assert not writer.is_alive()
 
 
 def test_pipelined_launch_whose_record_fails_is_dropped(env):

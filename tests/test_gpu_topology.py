@@ -167,6 +167,24 @@ def test_visible_devices_restrict_and_renumber(tmp_path):
     assert G.discover(env={"HIP_VISIBLE_DEVICES": ""}, fixture_dir=node).count == 8   # empty = unset
 
 
+def test_visible_devices_by_uuid(tmp_path, caplog):
+    """ROCm also takes ``GPU-<unique id>`` entries: they select the device with that KFD
+    unique id; an entry no device matches leaves the inventory unfiltered, with a warning, instead
+    of advertising zero GPUs."""
+    node = _node(tmp_path, [0xA1] * 4 + [0xB2] * 4)
+    full = G.discover(env={}, fixture_dir=node)
+    u3, u6 = full.devices[3].unique_id, full.devices[6].unique_id
+    assert u3 and u6
+    inv = G.discover(env={"HIP_VISIBLE_DEVICES": f"GPU-{u6},GPU-{u3.upper()}"}, fixture_dir=node)
+    assert [d.kfd_node for d in inv.devices] == [full.devices[6].kfd_node, full.devices[3].kfd_node]
+    assert [d.index for d in inv.devices] == [0, 1]
+    mixed = G.discover(env={"ROCR_VISIBLE_DEVICES": f"1,GPU-{u6}"}, fixture_dir=node)
+    assert [d.kfd_node for d in mixed.devices] == [full.devices[1].kfd_node, full.devices[6].kfd_node]
+    with caplog.at_level("WARNING"):
+        unknown = G.discover(env={"HIP_VISIBLE_DEVICES": "GPU-deadbeefdeadbeef"}, fixture_dir=node)
+    assert unknown.count == 8 and "cannot identify" in caplog.text
+
+
 @pytest.mark.skipif(not os.path.isdir(BOX_FIXTURE), reason="no recorded MI355X box dump")
 def test_recorded_mi355x_box_dump():
     """The dump of the MI355X box (one GPU granted of its node's eight): only the granted GPU's KFD

@@ -2,8 +2,8 @@
 
 Every step's ACCEPT follows its durable record and the ACCEPTs keep step order; steps queued while
 a write is in flight are recorded together; a failed record drops its steps' operations (reported
-by ``drain``); ``drain`` returns only when everything submitted was recorded and sent, and the
-writer thread is gone. A ZooKeeper-backed DefaultScheduler turns it on by default
+by ``drain``); ``drain`` returns only when everything submitted was recorded and sent. One writer
+thread serves every cycle (parked in between) until ``close``. A ZooKeeper-backed DefaultScheduler turns it on by default
 (``SDK_PIPELINE_LAUNCH_WRITES``); a local persister keeps the inline writes.
 """
 import threading
@@ -31,6 +31,7 @@ def test_accepts_follow_their_record_in_order_and_coalesce():
     assert log == [("record", ["a1", "a2"]), ("send", ["a1", "a2"]),
                    ("record", ["b", "c", "d"]), ("send", ["b"]), ("send", ["c"]), ("send", ["d"])]
     assert p.writes == 2
+    p.close()
     assert not any(t.name == "launch-writer" for t in threading.enumerate())
 
 
@@ -39,8 +40,23 @@ def test_failed_record_drops_the_operations():
     p = LaunchPipeline(lambda recs: "bad" not in recs)
     p.submit(["bad"], sent.append)
     assert p.drain() == [["bad"]] and sent == []
-    p.submit(["ok"], sent.append)          # the next cycle starts a new writer
+    p.submit(["ok"], sent.append)          # the next cycle reuses the parked writer
     assert p.drain() == [] and sent == [["ok"]]
+    assert p.threads_started == 1
+    p.close()
+
+
+def test_one_writer_thread_serves_every_cycle_until_close():
+    """a writer per cycle gave a sync-call v1 driver one new master connection per cycle."""
+    seen = set()
+    p = LaunchPipeline(lambda recs: seen.add(threading.get_ident()) or True, name="launch-writer-test")
+    for cycle in range(20):
+        p.submit([cycle], lambda recs: None)
+        assert p.drain() == []
+    assert p.threads_started == 1 and len(seen) == 1
+    assert any(t.name == "launch-writer-test" for t in threading.enumerate())   # parked, not gone
+    p.close()
+    assert not any(t.name == "launch-writer-test" for t in threading.enumerate())
 
 
 def test_record_exception_is_a_failed_record():
@@ -49,6 +65,7 @@ def test_record_exception_is_a_failed_record():
     p = LaunchPipeline(record)
     p.submit(["x"], lambda recs: None)
     assert p.drain() == [["x"]]
+    p.close()
 
 
 def test_drain_without_submissions_returns_at_once():

@@ -85,6 +85,44 @@ def test_run_exit_codes_timeout_and_missing_program(launcher, tmp_path):
     assert launcher.run(["/no/such/program"], str(tmp_path), ENV, 5) == 127
 
 
+def test_tasks_get_default_sigpipe_and_sigxfsz(launcher, tmp_path):
+    """The helper ignores SIGPIPE for itself; its children must not inherit that: a
+    task's SigIgn mask has neither bit, and a pipeline's producer dies of SIGPIPE as under Popen."""
+    p, exits, done = _launch(launcher, tmp_path, "grep SigIgn /proc/self/status; "
+                                                 "yes | head -1 > /dev/null; echo \"${PIPESTATUS[0]}\"")
+    assert done.wait(10) and exits[0][1] == 0
+    sigign_line, producer_rc = (tmp_path / "stdout").read_text().split("\n")[:2]
+    mask = int(sigign_line.split()[1], 16)
+    assert not mask & (1 << (signal.SIGPIPE - 1)) and not mask & (1 << (signal.SIGXFSZ - 1))
+    assert int(producer_rc) == 128 + signal.SIGPIPE
+
+
+def test_send_failure_after_the_helper_died_is_reported_once(binary, tmp_path):
+    """The helper dies between a launch's registration and its send: the read loop reports it
+    through ``on_error``; the launch then returns instead of raising a second failure."""
+    nl = NativeLauncher(binary)
+    errors = []
+    orig = nl._send
+
+    def send_after_death(msg):
+        nl.proc.kill()
+        nl.proc.wait(5)
+        deadline = time.time() + 5
+        while not nl.closed and time.time() < deadline:   # the read loop saw EOF and failed the entry
+            time.sleep(0.01)
+        orig(msg)
+    nl._send = send_after_death
+    try:
+        p = nl.launch(["x", "-c", "true"], "/bin/bash", str(tmp_path), ENV, "", "", lambda proc, rc: None,
+                      on_error=lambda proc, msg: errors.append(msg))
+        assert len(errors) == 1 and p.pid == 0
+    except OSError:
+        # the entry was still registered when the send failed: raising is then the only report
+        assert errors == []
+    finally:
+        nl.close()
+
+
 def test_many_concurrent_runs(launcher, tmp_path):
     out = [None] * 32
 
