@@ -45,6 +45,16 @@ def parse_args(argv=None):
     ap.add_argument("--reference-steps", type=int, default=None,
                     help="cycles of the reference's unchanged gpu_resource.yml (default serial deploy) run after "
                          "the timed region and reported as `reference_spec` (default: --steps; 0 = skip)")
+    ap.add_argument("--topology", default="split", choices=["split", "inprocess"],
+                    help="split: the master and every agent's task lifecycle run in processes of their own (a "
+                         "master process; each rank, or a helper process per agent, runs its tasks), the "
+                         "scheduler here over the framed v1 stream; inprocess: one interpreter holds all of it")
+    ap.add_argument("--agent0", default="thread", choices=["thread", "process"],
+                    help="split topology without torchrun: agent 0 runs on a thread of this process (thread) or in "
+                         "a helper process like the others (process)")
+    ap.add_argument("--cluster-switch-interval-ms", type=float, default=0.0,
+                    help="split topology: interpreter switch interval of the master and agent processes "
+                         "(0: Python's 5 ms)")
     ap.add_argument("--verbose", action="store_true")
     args = ap.parse_args(argv)
     if args.reference_steps is None:
@@ -86,6 +96,13 @@ def main(argv=None) -> int:
     local_world = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
     cpus = [] if args.no_pin else pin_cpus(local_rank, local_world)
 
+    cluster = None
+    if args.topology == "split":
+        # before anything initialises a GPU: such a process may not start programs
+        from dcos_commons_amd.benchmarks.split_cluster import SplitCluster
+
+        cluster = SplitCluster.start(args, rank, world)
+
     import torch
 
     use_gpu = torch.cuda.is_available() and not args.no_gpu_probe
@@ -103,7 +120,12 @@ def main(argv=None) -> int:
 
     from dcos_commons_amd.benchmarks.runner import run_bench
 
-    result = run_bench(args, rank=rank, world=world, local_rank=local_rank, use_gpu=use_gpu, dist=dist)
+    try:
+        result = run_bench(args, rank=rank, world=world, local_rank=local_rank, use_gpu=use_gpu, dist=dist,
+                           cluster=cluster)
+    finally:
+        if cluster is not None:
+            cluster.close()
     if rank == 0 and result:
         result["config"]["cpus_per_rank"] = len(cpus) if cpus else None
     if rank == 0:

@@ -99,14 +99,60 @@ def agent_spec_from_registration(info: Dict, index: int) -> AgentSpec:
                                         devices=list(info["devices"]), cpus=16, mem=65536, disk=100000)
 
 
+class _LocalCluster:
+    """This interpreter's LocalMaster (agents' task lifecycles included)."""
+
+    def __init__(self, master: LocalMaster):
+        self.master = master
+
+    def driver(self, sched, info):
+        return LocalSchedulerDriver(self.master, sched, info)
+
+    def placement(self):
+        return self.master.placement()
+
+    def fail_task(self, task_id: str) -> None:
+        self.master.fail_task(task_id)
+
+    def shutdown(self) -> None:
+        self.master.shutdown()
+
+
+class _RemoteCluster:
+    """A fresh master in the master process (``mesos.master_process``), same agents."""
+
+    def __init__(self, client, allocation_interval_s: float):
+        from dcos_commons_amd.mesos.stream_api import StreamSchedulerDriver
+
+        self.client = client
+        self.address = client.call("reset", allocation_interval_s=allocation_interval_s)["stream"]
+        self._driver_cls = StreamSchedulerDriver
+
+    def driver(self, sched, info):
+        return self._driver_cls(self.address, sched, info)
+
+    def placement(self):
+        return self.client.call("placement")
+
+    def fail_task(self, task_id: str) -> None:
+        self.client.call("fail_task", task_id=task_id)
+
+    def shutdown(self) -> None:
+        pass
+
+
 class DeployBench:
     def __init__(self, n_agents: int, profile: str = "mi355x", spec_file: str = "gpu.yml",
                  check_runner: Optional[Callable[[P.TaskInfo, List[int]], bool]] = None,
                  gpu_devices: Optional[List[int]] = None, allocation_interval_s: float = 1.0,
                  timeout_s: float = 120.0, agent_runners: Optional[List[Callable]] = None,
                  extra_env: Optional[Dict[str, str]] = None, agent_specs: Optional[List[AgentSpec]] = None,
-                 spec_env: Optional[Dict[str, str]] = None):
+                 spec_env: Optional[Dict[str, str]] = None, master_client=None):
         self.n = n_agents
+        # ``mesos.master_process.MasterClient``: the master runs in a process of its own and the
+        # agents run their tasks themselves (the scheduler subscribes over ``mesos.stream_api``);
+        # None: the master and every agent's task lifecycle run in this interpreter
+        self.master_client = master_client
         self.extra_env = dict(extra_env or {})  # scheduler flag overrides on top of the profile
         self.spec_env = dict(spec_env or {})    # spec rendering overrides (e.g. WORLD_COUNT)
         self.profile = profile
@@ -114,16 +160,17 @@ class DeployBench:
         self.spec_file = spec_file
         self.check_runner = check_runner
         self.gpu_devices = gpu_devices if gpu_devices is not None else list(range(n_agents))
-        self.agent_specs = agent_specs if agent_specs is not None else agent_specs_from_inventory(self.gpu_devices)
-        if len(self.agent_specs) != n_agents:
+        self.agent_specs = agent_specs if agent_specs is not None else (
+            [] if master_client is not None else agent_specs_from_inventory(self.gpu_devices))
+        if master_client is None and len(self.agent_specs) != n_agents:
             raise ValueError(f"{len(self.agent_specs)} agent specs for {n_agents} agents")
         self.last_placement: List[Dict] = []  # LocalMaster.placement() once the last deploy completed
         self.allocation_interval_s = allocation_interval_s
         self.timeout_s = timeout_s
         self.agent_runners = agent_runners  # per-agent check runner (remote GPU agents)
         # the agents' check executors outlive a cycle, as they outlive a scheduler on a real cluster
-        self.behavior = TaskBehavior(TaskTiming(), check_runner=self.check_runner,
-                                     check_workers=max(8, n_agents)).prestart()
+        self.behavior = None if master_client is not None else TaskBehavior(
+            TaskTiming(), check_runner=self.check_runner, check_workers=max(8, n_agents)).prestart()
 
     # -- helpers ---------------------------------------------------------------------------
     def _wait(self, pred, what: str, event=None) -> float:
@@ -170,11 +217,13 @@ class DeployBench:
         if r.status != 200:
             raise RuntimeError(f"/v1/plans/{plan} answered {r.status} after the plan completed")
 
-    def _make_master(self) -> LocalMaster:
+    def _make_master(self) -> "_Cluster":
+        if self.master_client is not None:
+            return _RemoteCluster(self.master_client, self.allocation_interval_s)
         master = LocalMaster(allocation_interval_s=self.allocation_interval_s, behavior=self.behavior)
         for i, spec in enumerate(self.agent_specs):
             master.add_agent(spec, check_runner=self.agent_runners[i] if self.agent_runners else None)
-        return master
+        return _LocalCluster(master)
 
     # -- one cycle -------------------------------------------------------------------------
     def run_cycle(self) -> CycleResult:
@@ -202,7 +251,7 @@ class DeployBench:
                 marks.setdefault("subscribed", time.perf_counter())
                 return orig(*a, **k)
             sched.registered = registered
-            return LocalSchedulerDriver(master, sched, info)
+            return master.driver(sched, info)
         runner = SchedulerRunner(builder, driver_factory=driver_factory)
         try:
             t0 = time.perf_counter()

@@ -42,10 +42,16 @@ def _sched_env(args) -> dict:
     return dict(kv.split("=", 1) for kv in getattr(args, "sched_env", None) or [])
 
 
-def run_bench(args, rank: int, world: int, local_rank: int, use_gpu: bool, dist=None) -> dict:
+def run_bench(args, rank: int, world: int, local_rank: int, use_gpu: bool, dist=None, cluster=None) -> dict:
+    """``cluster``: the processes of the split topology (``split_cluster.SplitCluster``, started by
+    ``bench.py`` before any GPU was initialised); None runs the in-process topology."""
     n = args.gpus if world == 1 else world
     if world > 1 and args.gpus != world:
         raise SystemExit(f"--gpus {args.gpus} does not match WORLD_SIZE {world}")
+    if cluster is not None:
+        if world == 1:
+            return _run_single_split(args, n, use_gpu, cluster)
+        return _run_distributed_split(args, rank, world, local_rank, use_gpu, dist, cluster)
     if world == 1:
         return _run_single(args, n, use_gpu)
     return _run_distributed(args, rank, world, local_rank, use_gpu, dist)
@@ -99,7 +105,10 @@ def _reference_row(args, n, make_bench) -> dict:
         # the repository's rewrite of the same scenario (also no plans: -> serial)
         path = os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))),
                             "frameworks", "helloworld", "specs", "gpu_resource.yml")
-        which = "repo frameworks/helloworld/specs/gpu_resource.yml (no reference tree on this machine)"
+        which = ("repo frameworks/helloworld/specs/gpu_resource.yml: the reference scenario rewritten for this "
+                 "repository (no reference tree on this machine); it builds the same ServiceSpec as the reference's "
+                 "dist/gpu_resource.yml (tests/test_reference_conformance.py::"
+                 "test_repo_gpu_resource_builds_the_reference_scenario)")
     else:
         which = "reference frameworks/helloworld/src/main/dist/gpu_resource.yml, unchanged"
     bench = make_bench(path)
@@ -269,5 +278,152 @@ def _run_distributed(args, rank, world, local_rank, use_gpu, dist):
                      "elapsed_max_s": float(t.item())})
     out = _summary(args, world, cycles, float(t.item()), use_gpu, f"agents{world}-ranks{world}")
     out["config"]["agent_attributes"] = specs[0].attributes
+    out.update(extra)
+    return out
+
+
+# -- split topology: master process, agents that run their own tasks --------------------------
+def _agent_check(device: int, use_gpu: bool, checks: list):
+    """``check(msg)`` of this process's agent (its device): the HIP probe or a synthetic pass;
+    every check is recorded as (assigned devices, device, ok)."""
+    local = gpu_check_runner() if use_gpu else None
+
+    def check(msg):
+        assigned = list(msg.get("devices") or [device])
+        if assigned != [device]:
+            # the master assigns from the devices this agent registered: anything else is a bug
+            checks.append((assigned, device, False))
+            return False, f"check for devices {assigned} sent to the agent of device {device}"
+        ok = True if local is None else local(None, [device])
+        checks.append((assigned, device, bool(ok)))
+        return ok, f"{'probe' if local is not None else 'synthetic'} on device {device}"
+    return check
+
+
+def _start_agent_thread(host: str, port: int, info: dict, check):
+    import threading
+
+    from dcos_commons_amd.parallel import agent_link
+
+    registered = threading.Event()
+    t = threading.Thread(target=agent_link.run_agent, args=(host, port, info, check),
+                         kwargs={"on_registered": registered.set}, name="agent-link", daemon=True)
+    t.start()
+    if not registered.wait(120):
+        raise TimeoutError("this process's agent did not register with the master process")
+    return t
+
+
+def _split_summary(args, n, cycles, elapsed, use_gpu, parallelism, infos):
+    out = _summary(args, n, cycles, elapsed, use_gpu, parallelism)
+    out["config"]["topology"] = ("split: master process; each agent (rank or helper process) runs its tasks' "
+                                 "lifecycle and readiness checks; scheduler over the framed v1 stream")
+    out["config"]["agent_attributes"] = agent_spec_from_registration(infos[0], 0).attributes
+    return out
+
+
+def _run_single_split(args, n, use_gpu, cluster):
+    import torch
+
+    from dcos_commons_amd.mesos.master_process import MasterClient
+
+    ndev = torch.cuda.device_count() if use_gpu else 1
+    checks: list = []
+    info = _local_agent_info(0, 0, 0)
+    agent = None
+    if getattr(args, "agent0", "thread") == "thread":
+        agent = _start_agent_thread(cluster.host, cluster.ports["agents"], info, _agent_check(0, use_gpu, checks))
+    client = MasterClient(cluster.host, cluster.ports["control"])
+    infos = client.call("agents", n=n)
+
+    def make(spec_file="gpu.yml", spec_env=None):
+        return DeployBench(n, profile=args.profile, allocation_interval_s=args.allocation_interval,
+                           extra_env=_sched_env(args), spec_file=spec_file, spec_env=spec_env, master_client=client)
+    bench = make()
+    for _ in range(args.warmup):
+        bench.run_cycle()
+    _sync()
+    t0 = time.perf_counter()
+    cycles = [bench.run_cycle() for _ in range(args.steps)]
+    _sync()
+    elapsed = time.perf_counter() - t0
+    out = _split_summary(args, n, cycles, elapsed, use_gpu, f"agents{n}", infos)
+    out["config"]["agent_processes"] = n
+    out["config"]["devices"] = [i % max(1, ndev) for i in range(n)]
+    placement = bench.last_placement
+    out.update(_reference_row(args, n, lambda path: make(path, REFERENCE_ROW_ENV)))
+    client.call("shutdown")
+    if agent is not None:
+        agent.join(10)
+    _record(os.environ.get("SDK_BENCH_RECORD"), {"rank": 0, "placement": placement, "registered": info,
+                                                 "checks": checks, "agents": infos})
+    return out
+
+
+def _run_distributed_split(args, rank, world, local_rank, use_gpu, dist, cluster):
+    import torch
+
+    from dcos_commons_amd.mesos.master_process import MasterClient
+
+    box = [cluster.ports if cluster is not None and rank == 0 else None]
+    dist.broadcast_object_list(box, src=0)
+    ports = box[0]
+    host = os.environ.get("MASTER_ADDR", "127.0.0.1")
+    if torch.cuda.is_available():
+        n_dev = torch.cuda.device_count()
+    else:
+        from dcos_commons_amd.ops import gpu as G
+
+        n_dev = G.node_inventory(1).count
+    device = local_rank % max(n_dev, 1)
+    coll_dev = "cuda" if torch.cuda.is_available() and getattr(args, "dist_backend", "nccl") == "nccl" else "cpu"
+    record = os.environ.get("SDK_BENCH_RECORD")
+    checks: list = []
+    info = _local_agent_info(rank, local_rank, device)
+    agent = _start_agent_thread(host, ports["agents"], info, _agent_check(device, use_gpu, checks))
+
+    def barrier():
+        _sync()
+        dist.barrier()
+
+    if rank != 0:
+        # this rank is an agent: its runtime serves launches and checks on its own threads while
+        # the main thread marks the timed window between rank 0's barriers
+        barrier()
+        t0 = time.perf_counter()
+        barrier()
+        elapsed = time.perf_counter() - t0
+        t = torch.tensor([elapsed], dtype=torch.float64, device=coll_dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        agent.join()    # until the master process shuts the agents down
+        _record(record, {"rank": rank, "device": device, "registered": info, "checks": checks,
+                         "elapsed_local_s": elapsed, "elapsed_max_s": float(t.item())})
+        return {}
+
+    client = MasterClient(cluster.host, ports["control"])
+    infos = client.call("agents", n=world)
+
+    def make(spec_file="gpu.yml", spec_env=None):
+        return DeployBench(world, profile=args.profile, allocation_interval_s=args.allocation_interval,
+                           extra_env=_sched_env(args), spec_file=spec_file, spec_env=spec_env, master_client=client)
+    bench = make()
+    for _ in range(args.warmup):
+        bench.run_cycle()
+    barrier()
+    t0 = time.perf_counter()
+    cycles = [bench.run_cycle() for _ in range(args.steps)]
+    barrier()
+    elapsed = time.perf_counter() - t0
+    placement = bench.last_placement
+    extra = _reference_row(args, world, lambda path: make(path, REFERENCE_ROW_ENV))
+    t = torch.tensor([elapsed], dtype=torch.float64, device=coll_dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    client.call("shutdown")
+    agent.join(30)
+    specs = [agent_spec_from_registration(x, i) for i, x in enumerate(infos)]
+    _record(record, {"rank": 0, "device": device, "registered": info, "checks": checks, "placement": placement,
+                     "agents": [_spec_view(s) for s in specs], "elapsed_local_s": elapsed,
+                     "elapsed_max_s": float(t.item())})
+    out = _split_summary(args, world, cycles, float(t.item()), use_gpu, f"agents{world}-ranks{world}", infos)
     out.update(extra)
     return out

@@ -100,6 +100,43 @@ class _Subscription:
             self.queue.put(_CLOSE)
 
 
+def apply_call(m: LocalMaster, fid: str, call: P.Call, sub) -> int:
+    """Applies one v1 scheduler ``Call`` of framework ``fid`` (already authenticated to its
+    subscription ``sub``) to the master: 202, or 400 for a call type a scheduler may not send.
+    Shared by the HTTP front end and the framed stream front end (``mesos.stream_api``)."""
+    t = call.type
+    if t == P.Call.ACCEPT:
+        refuse = call.accept.filters.refuse_seconds if call.accept.HasField("filters") else 5.0
+        m.accept(fid, [o.value for o in call.accept.offer_ids], list(call.accept.operations), refuse)
+    elif t == P.Call.DECLINE:
+        refuse = call.decline.filters.refuse_seconds if call.decline.HasField("filters") else 5.0
+        m.decline(fid, [o.value for o in call.decline.offer_ids], refuse)
+    elif t == P.Call.REVIVE:
+        m.revive(fid)
+    elif t == P.Call.SUPPRESS:
+        m.suppress(fid)
+    elif t == P.Call.KILL:
+        m.kill(fid, call.kill.task_id.value)
+    elif t == P.Call.RECONCILE:
+        statuses = []
+        for task in call.reconcile.tasks:
+            s = P.TaskStatus()
+            s.task_id.CopyFrom(task.task_id)
+            if task.HasField("agent_id"):
+                s.agent_id.CopyFrom(task.agent_id)
+            statuses.append(s)
+        m.reconcile(fid, statuses)
+    elif t == P.Call.ACKNOWLEDGE:
+        sub.acknowledged.append(call.acknowledge.uuid)
+    elif t == P.Call.TEARDOWN:
+        m.teardown(fid)
+    elif t in (P.Call.MESSAGE, P.Call.REQUEST, P.Call.SHUTDOWN):
+        pass
+    else:
+        return 400
+    return 202
+
+
 class HttpMaster:
     def __init__(self, master: LocalMaster, host: str = "127.0.0.1", port: int = 0,
                  heartbeat_s: float = 15.0, redirect_to: Optional[str] = None):
@@ -202,40 +239,12 @@ class HttpMaster:
         if sub is None or stream_id != sub.stream_id:
             return 400
         self._count(call.type)
-        m, t = self.master, call.type
-        if t == P.Call.ACCEPT:
-            refuse = call.accept.filters.refuse_seconds if call.accept.HasField("filters") else 5.0
-            m.accept(fid, [o.value for o in call.accept.offer_ids], list(call.accept.operations), refuse)
-        elif t == P.Call.DECLINE:
-            refuse = call.decline.filters.refuse_seconds if call.decline.HasField("filters") else 5.0
-            m.decline(fid, [o.value for o in call.decline.offer_ids], refuse)
-        elif t == P.Call.REVIVE:
-            m.revive(fid)
-        elif t == P.Call.SUPPRESS:
-            m.suppress(fid)
-        elif t == P.Call.KILL:
-            m.kill(fid, call.kill.task_id.value)
-        elif t == P.Call.RECONCILE:
-            statuses = []
-            for task in call.reconcile.tasks:
-                s = P.TaskStatus()
-                s.task_id.CopyFrom(task.task_id)
-                if task.HasField("agent_id"):
-                    s.agent_id.CopyFrom(task.agent_id)
-                statuses.append(s)
-            m.reconcile(fid, statuses)
-        elif t == P.Call.ACKNOWLEDGE:
-            sub.acknowledged.append(call.acknowledge.uuid)
-        elif t == P.Call.TEARDOWN:
-            m.teardown(fid)
+        code = apply_call(self.master, fid, call, sub)
+        if call.type == P.Call.TEARDOWN:
             with self._lock:
                 self.subscriptions.pop(fid, None)
             sub.close()
-        elif t in (P.Call.MESSAGE, P.Call.REQUEST, P.Call.SHUTDOWN):
-            pass
-        else:
-            return 400
-        return 202
+        return code
 
     def state(self) -> dict:
         def do():

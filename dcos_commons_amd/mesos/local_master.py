@@ -211,6 +211,7 @@ class _Task:
     epoch: int = 0  # bumps on kill/failure so stale timers are ignored
     # the task's addresses as its statuses report them (``container_status.network_infos``)
     networks: List[P.NetworkInfo] = field(default_factory=list)
+    reported_exit: bool = False   # its end came from its agent's runtime (no ``drop`` to send back)
 
 
 @dataclass
@@ -239,6 +240,9 @@ class _Agent:
         self.index = 0            # position among the master's agents (overlay subnet 9.0.<index>.0/24)
         self._overlay_ips = itertools.count(2)
         self._check_thread = None  # the agent's own thread for inline checks (see check_thread)
+        # the agent runs its tasks' lifecycle itself (``mesos.agent_runtime``): an object whose
+        # ``send(msg)`` reaches it; its reports come back through ``LocalMaster.runtime_reports``
+        self.runtime = None
 
     def check_thread(self):
         """This agent's check executor: one thread, as a Mesos agent's executor runs its tasks'
@@ -408,11 +412,15 @@ class LocalMaster:
         self._listeners.append(fn)
 
     # -- cluster management --------------------------------------------------------------
-    def add_agent(self, spec: AgentSpec, check_runner=None) -> str:
+    def add_agent(self, spec: AgentSpec, check_runner=None, runtime=None) -> str:
+        """``runtime``: the agent runs its tasks' lifecycle and checks itself (an object with
+        ``send(msg)``, see ``mesos.agent_runtime``); the master then only applies ACCEPTs, keeps
+        the books and turns the agent's reports into status updates."""
         def do():
             aid = f"agent-{len(self.agents)}-{uuid.uuid4().hex[:6]}"
             self.agents[aid] = _Agent(aid, spec)
             self.agents[aid].check_runner = check_runner
+            self.agents[aid].runtime = runtime
             self.agents[aid].index = len(self.agents)
             self._allocate()
             return aid
@@ -457,6 +465,12 @@ class LocalMaster:
             t = self._find_task(task_id)
             if t is None:
                 raise KeyError(task_id)
+            a = self.agents.get(t.agent_id)
+            if a is not None and a.runtime is not None and t.status.state not in TERMINAL:
+                # the task dies on its agent, which reports it (as an executor would)
+                a.runtime.send({"op": "fail", "task": task_id, "state": state, "message": message,
+                                "reason": P.TaskStatus.REASON_COMMAND_EXECUTOR_FAILED})
+                return
             self._update(t, state, message=message, reason=P.TaskStatus.REASON_COMMAND_EXECUTOR_FAILED)
         self.call(do)
 
@@ -924,9 +938,68 @@ class LocalMaster:
                 agent.executors[key].tasks.add(t.task_id.value)
             if self._executes:
                 self.behavior.launch(self, task, agent)
+            elif agent.runtime is not None:
+                agent.runtime.send(self._runtime_launch(task, self.behavior.timing(t)))
             else:
                 timing = self.behavior.timing(t)
                 self._schedule(timing.starting_s, self._lifecycle_starting, task, task.epoch, timing)
+
+    # -- agent-run lifecycle (mesos.agent_runtime) ------------------------------------------
+    @staticmethod
+    def _runtime_launch(task: _Task, timing: TaskTiming) -> dict:
+        info = task.info
+        check = None
+        if info.HasField("check"):
+            check = {"delay": info.check.delay_seconds if timing.honor_check_delays else 0.0,
+                     "interval": info.check.interval_seconds or 1.0}
+        return {"op": "launch", "task": info.task_id.value, "name": info.name, "devices": list(task.gpu_devices),
+                "check": check, "health": info.HasField("health_check"),
+                "timing": {"starting": timing.starting_s, "running": timing.running_s,
+                           "check_exec": timing.check_exec_s, "finish_after": timing.finish_after_s,
+                           "exit_state": timing.exit_state}}
+
+    def runtime_reports(self, agent_id: str, reports: List[dict]) -> None:
+        """What an agent running its own tasks reported (any thread): applied in order on the
+        dispatcher thread as the status updates Mesos would forward."""
+        self._schedule(0, self._apply_runtime_reports, agent_id, list(reports))
+
+    def _apply_runtime_reports(self, agent_id: str, reports: List[dict]) -> None:
+        a = self.agents.get(agent_id)
+        for r in reports:
+            t = a.tasks.get(r.get("task")) if a is not None else None
+            if t is None or t.status.state in TERMINAL:
+                continue
+            ev = r.get("event")
+            if ev == "starting":
+                self._update(t, P.TASK_STARTING)
+            elif ev == "running":
+                extra = {}
+                if t.info.HasField("check"):
+                    cs = P.CheckStatusInfo(type=t.info.check.type)
+                    cs.command.SetInParent()
+                    extra["check_status"] = cs
+                if t.info.HasField("health_check"):
+                    extra["healthy"] = True
+                self._update(t, P.TASK_RUNNING, **extra)
+            elif ev == "ready":
+                self._lifecycle_ready(t, t.epoch)
+            elif ev == "check_failed":
+                if t.status.state != P.TASK_RUNNING:
+                    continue
+                prev = t.status.check_status.command.exit_code if t.status.HasField("check_status") else None
+                if prev != 1:
+                    cs = P.CheckStatusInfo(type=t.info.check.type)
+                    cs.command.exit_code = 1
+                    self._update(t, P.TASK_RUNNING, check_status=cs,
+                                 reason=P.TaskStatus.REASON_TASK_CHECK_STATUS_UPDATED)
+            elif ev == "exited":
+                t.reported_exit = True
+                fields = {"message": r.get("message", "")}
+                if r.get("reason") is not None:
+                    fields["reason"] = int(r["reason"])
+                self._update(t, int(r.get("state", P.TASK_FINISHED)), **fields)
+            else:
+                LOGGER.warning("unknown agent report %r", r)
 
     # -- task lifecycle ----------------------------------------------------------------
     def _lifecycle_starting(self, task: _Task, epoch: int, timing: TaskTiming) -> None:
@@ -1086,6 +1159,10 @@ class LocalMaster:
             return
         if self._executes and self.behavior.kill(self, t):
             return  # TASK_KILLED is reported when the process has exited
+        a = self.agents.get(t.agent_id)
+        if a is not None and a.runtime is not None:
+            a.runtime.send({"op": "kill", "task": task_id})
+            return  # the agent reports TASK_KILLED once it has stopped the task
         self._update(t, P.TASK_KILLED, message="Task killed by scheduler")
 
     def _find_task(self, task_id: str) -> Optional[_Task]:
@@ -1133,6 +1210,9 @@ class LocalMaster:
         a = self.agents.get(task.agent_id)
         if a is None:
             return
+        if a.runtime is not None and not task.reported_exit:
+            # ended by the master (teardown, forget, agent removed): the agent stops tracking it
+            a.runtime.send({"op": "drop", "task": task.info.task_id.value})
         for r in task.resources:
             a.available.add(r)
         task.resources = []

@@ -9,9 +9,10 @@ pod readiness). Wire format: newline-delimited JSON, request ids for request/res
 The listener binds to loopback (127.0.0.1) by default: the single-node benchmark and tests never
 need more, and the link carries no authentication.
 
-Ops (master -> agent): ``check`` {id, task, name, devices}, ``barrier`` {id}, ``shutdown``.
-Ops (agent -> master): ``register`` {hostname, gpus, devices, attributes, rank},
-``result`` {id, ok, detail}.
+Ops (master -> agent): ``check`` {id, task, name, devices}, ``barrier`` {id}, ``shutdown``, and
+for an agent that runs its tasks' lifecycle itself (``mesos.agent_runtime``) ``launch``, ``kill``,
+``fail``, ``drop``, ``reset`` (no reply). Ops (agent -> master): ``register`` {hostname, gpus,
+devices, attributes, rank}, ``result`` {id, ok, detail}, and unsolicited ``status`` {reports}.
 """
 from __future__ import annotations
 
@@ -61,6 +62,8 @@ class RemoteAgent:
         self._pending: Dict[int, Future] = {}
         self._lock = threading.Lock()
         self.alive = True
+        # unsolicited ``status`` messages of an agent running its own tasks (agent_runtime reports)
+        self.on_status: Callable[[List[dict]], None] = lambda reports: None
         self._reader = threading.Thread(target=self._read_loop, daemon=True, name=f"agent-link-{info.get('rank')}")
         self._reader.start()
 
@@ -76,6 +79,12 @@ class RemoteAgent:
                 msg = None
             if msg is None:
                 break
+            if msg.get("op") == "status":
+                try:
+                    self.on_status(msg.get("reports") or [])
+                except Exception:  # noqa: BLE001
+                    LOGGER.exception("agent status reports failed")
+                continue
             with self._lock:
                 fut = self._pending.pop(msg.get("id"), None)
             if isinstance(fut, Future):
@@ -134,6 +143,13 @@ class RemoteAgent:
         self.request_async("check", lambda r: done(bool(r.get("ok"))), task=task_info.task_id.value,
                            name=task_info.name, devices=devices)
 
+
+    def send(self, msg: dict) -> None:
+        """A runtime message (``launch``, ``kill``, ...): no reply; a dead link is logged."""
+        try:
+            self.conn.send(msg)
+        except OSError as e:
+            LOGGER.warning("agent link to rank %s: %s dropped (%s)", self.rank, msg.get("op"), e)
 
     def shutdown(self) -> None:
         try:
@@ -223,9 +239,17 @@ class AgentLinkServer:
             pass
 
 
+RUNTIME_OPS = ("launch", "kill", "fail", "drop", "reset")
+
+
 def run_agent(master_host: str, port: int, info: dict, check: Callable[[dict], tuple],
-              on_barrier: Optional[Callable[[], None]] = None) -> None:
-    """Agent main loop (blocking): register, then serve ``check`` / ``barrier`` until shutdown."""
+              on_barrier: Optional[Callable[[], None]] = None, on_registered: Optional[Callable[[], None]] = None
+              ) -> None:
+    """Agent main loop (blocking): register, then serve until shutdown: ``check`` / ``barrier``
+    requests, and the runtime messages of the tasks this agent runs itself (``agent_runtime``:
+    their checks call ``check({"devices": ...})`` on this process's GPU)."""
+    from dcos_commons_amd.mesos.agent_runtime import AgentRuntime
+
     s = socket.create_connection((master_host, port), timeout=120)
     s.settimeout(None)
     s.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
@@ -234,22 +258,37 @@ def run_agent(master_host: str, port: int, info: dict, check: Callable[[dict], t
     ack = conn.recv()
     if not ack or ack.get("op") != "registered":
         raise ConnectionError("agent registration rejected")
-    while True:
-        msg = conn.recv()
-        if msg is None or msg.get("op") == "shutdown":
-            break
-        op, rid = msg.get("op"), msg.get("id")
-        if op == "check":
-            try:
-                ok, detail = check(msg)
-            except Exception as e:  # noqa: BLE001
-                LOGGER.exception("check failed")
-                ok, detail = False, str(e)
-            conn.send({"op": "result", "id": rid, "ok": bool(ok), "detail": detail})
-        elif op == "barrier":
-            conn.send({"op": "result", "id": rid, "ok": True})
-            if on_barrier is not None:
-                on_barrier()
-        else:
-            conn.send({"op": "result", "id": rid, "ok": False, "detail": f"unknown op {op}"})
-    conn.close()
+    if on_registered is not None:
+        on_registered()
+
+    def report(reports):
+        try:
+            conn.send({"op": "status", "id": 0, "reports": reports})
+        except OSError as e:
+            LOGGER.warning("agent status reports lost: %s", e)
+    runtime = AgentRuntime(report, lambda devices: bool(check({"devices": devices})[0]),
+                           name=f"agent-runtime-{info.get('rank', 0)}")
+    try:
+        while True:
+            msg = conn.recv()
+            if msg is None or msg.get("op") == "shutdown":
+                break
+            op, rid = msg.get("op"), msg.get("id")
+            if op in RUNTIME_OPS:
+                runtime.handle(msg)
+            elif op == "check":
+                try:
+                    ok, detail = check(msg)
+                except Exception as e:  # noqa: BLE001
+                    LOGGER.exception("check failed")
+                    ok, detail = False, str(e)
+                conn.send({"op": "result", "id": rid, "ok": bool(ok), "detail": detail})
+            elif op == "barrier":
+                conn.send({"op": "result", "id": rid, "ok": True})
+                if on_barrier is not None:
+                    on_barrier()
+            else:
+                conn.send({"op": "result", "id": rid, "ok": False, "detail": f"unknown op {op}"})
+    finally:
+        runtime.shutdown()
+        conn.close()

@@ -142,3 +142,38 @@ def test_deploy_bench_waits_on_status_events():
     waited = b._wait(pred, "test", ev)
     assert state["done"] and 0.04 < waited < 1.0
     assert state["checks"] < 30          # woken by the event / 5 ms ticks, not a 1 ms poll loop
+
+
+@pytest.mark.timeout(300)
+def test_bench_single_process_with_agent_processes(tmp_path):
+    """``--gpus 3`` without torchrun: the master process plus two helper agent processes
+    (``parallel.agent_process``); the bench process is agent 0. One pod per agent."""
+    record = tmp_path / "record"
+    env = dict(os.environ, PYTHONPATH=ROOT, SDK_BENCH_RECORD=str(record))
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "3", "--steps", "1", "--warmup", "1",
+                        "--no-gpu-probe", "--allocation-interval", "0.05", "--reference-steps", "1"],
+                       capture_output=True, text=True, timeout=280, env=env, cwd=ROOT)
+    assert p.returncode == 0, p.stderr[-3000:]
+    recs = _json_lines(p.stdout)
+    assert len(recs) == 1
+    rec = recs[0]
+    _check(rec, 3, 1, 1)
+    assert rec["config"]["topology"].startswith("split") and rec["config"]["agent_processes"] == 3
+    data = json.load(open(record / "rank0.json"))
+    assert sorted(a["rank"] for a in data["agents"]) == [0, 1, 2]
+    hosts = {a["hostname"] for a in data["agents"]}
+    placed = [x for x in data["placement"] if x["task"].startswith("hello-")]
+    assert len(placed) == 3 and {x["hostname"] for x in placed} == hosts     # hostname:UNIQUE, one per agent
+    assert data["checks"] and all(ok for _, _, ok in data["checks"])       # agent 0's checks ran here
+
+
+def test_bench_inprocess_topology():
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "1", "--warmup", "0",
+                        "--no-gpu-probe", "--allocation-interval", "0.05", "--topology", "inprocess",
+                        "--reference-steps", "0"],
+                       capture_output=True, text=True, timeout=240, env=env, cwd=ROOT)
+    assert p.returncode == 0, p.stderr[-2000:]
+    rec = _json_lines(p.stdout)[0]
+    _check(rec, 2, 1, 0)
+    assert "topology" not in rec["config"]

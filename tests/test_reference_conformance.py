@@ -193,3 +193,33 @@ def test_reference_hdfs_deploys_then_rolls_out_an_update():
      .run([Send.register(), Expect.that(update_selected, "update plan serves as deploy"),
            Send.drive_plan("deploy"), Expect.plan_status("deploy", Status.COMPLETE),
            Expect.that(relaunched, "every node relaunched")]))
+
+
+def _spec_json(spec_path: str) -> dict:
+    """The ServiceSpec ``spec_path`` builds when rendered with the reference helloworld package's
+    universe defaults (the strict rendering path), as JSON."""
+    import json
+
+    r = ServiceTestRunner(spec_path, universe_dir=os.path.join(HELLO, "universe")).set_scheduler_env(
+        SDK_REVIVE_INTERVAL_S="0")
+    _, spec, _, _ = r._build()
+    return json.loads(spec.to_json_string())
+
+
+def test_repo_gpu_resource_builds_the_reference_scenario():
+    """``frameworks/helloworld/specs/gpu_resource.yml`` (the spec the bench's ``reference_spec``
+    row runs where no reference tree exists) builds the same ServiceSpec as the reference's
+    unchanged ``dist/gpu_resource.yml``: same pods, resources, volumes, commands, health and
+    readiness checks, placement and default (serial) deploy. (The reference's pod-level
+    ``container:`` block is ignored by RawPod, so it contributes nothing to compare.)"""
+    repo_spec = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                             "frameworks", "helloworld", "specs", "gpu_resource.yml")
+    ours, theirs = _spec_json(repo_spec), _spec_json(os.path.join(DIST, "gpu_resource.yml"))
+    assert ours == theirs
+    pods = {p["type"]: p for p in ours["pod-specs"]}
+    hello, world = pods["hello"]["task-specs"][0], pods["world"]["task-specs"][0]
+    gpus = [r["value"]["scalar"]["value"] for r in hello["resource-set"]["resource-specifications"]
+            if r["name"] == "gpus"]
+    assert gpus == [1.0] and hello["health-check-spec"]
+    assert [v["container-path"] for v in hello["resource-set"]["volume-specifications"]] == ["hello-container-path"]
+    assert len(world["resource-set"]["volume-specifications"]) == 2 and world["readiness-check-spec"]
