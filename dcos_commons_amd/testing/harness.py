@@ -809,6 +809,9 @@ class ServiceTestRunner:
         sched_env = self.scheduler_environment()
         cfg_env = dict(sched_env) if self.universe_dir is not None else {}
         cfg_env.update({"PORT_API": "0", "SDK_EVENT_DRIVEN": "false", "SDK_OFFER_HOLD_S": "0"})
+        from dcos_commons_amd.testing import profiles
+
+        cfg_env.update(profiles.ACTIVE)     # the suite's flag profile; a test's own flags win
         cfg_env.update(self.scheduler_env)
         if "DCOS_SERVICE_ACCOUNT_CREDENTIAL" not in cfg_env:
             # the reference runner's mocked SchedulerConfig hands out a (null) token provider

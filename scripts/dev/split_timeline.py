@@ -1,0 +1,91 @@
+"""Per-span timeline of one traced deploy in the split topology (master process, one agent process
+per pod, scheduler here over the framed stream): python scripts/dev/split_timeline.py N [--probe].
+
+Prints the scheduler process's spans (offer cycle, evaluations, accepts, status batches) relative
+to the deploy's start, each with its thread's CPU time, and the scheduler threads' CPU shares."""
+import argparse
+import collections
+import os
+import subprocess
+import sys
+import threading
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+os.environ.setdefault("SDK_TRACE", "1")
+import logging  # noqa: E402
+
+logging.disable(logging.WARNING)
+from dcos_commons_amd import trace  # noqa: E402
+from dcos_commons_amd.mesos import master_process as MP  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("n", type=int)
+ap.add_argument("--probe", action="store_true")
+ap.add_argument("--cycles", type=int, default=5)
+args = ap.parse_args()
+
+proc, ports = MP.spawn()
+client = MP.MasterClient("127.0.0.1", ports["control"])
+root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+kids = [subprocess.Popen([sys.executable, "-m", "dcos_commons_amd.parallel.agent_process", "--port",
+                          str(ports["agents"]), "--rank", str(i), "--device", "0", "--probe",
+                          "on" if args.probe else "off"], cwd=root) for i in range(args.n)]
+client.call("agents", n=args.n)
+
+cpu = collections.defaultdict(float)
+lock = threading.Lock()
+orig_run = threading.Thread.run
+
+
+def run(self, *a, **k):
+    t0 = time.thread_time()
+    try:
+        return orig_run(self, *a, **k)
+    finally:
+        with lock:
+            cpu[self.name.split("-")[0] if self.name.startswith("Thread") else self.name] += time.thread_time() - t0
+
+
+threading.Thread.run = run
+import dcos_commons_amd.benchmarks.deploy_bench as DB  # noqa: E402
+
+_orig = DB.SchedulerRunner.run
+
+
+def _run(self, *a, **k):
+    trace.TRACER.instant("deploy_start")
+    return _orig(self, *a, **k)
+
+
+DB.SchedulerRunner.run = _run
+b = DB.DeployBench(args.n, master_client=client)
+for _ in range(3):
+    b.run_cycle()
+deploys = []
+for _ in range(args.cycles):
+    deploys.append(b.run_cycle().deploy_s)
+trace.TRACER.clear()
+r = b.run_cycle()
+time.sleep(0.3)
+print("deploy ms: traced %.2f; untraced-loop mean %.2f" % (r.deploy_s * 1e3, sum(deploys) / len(deploys) * 1e3))
+ev = sorted(trace.TRACER.events(), key=lambda e: e["ts"])
+t0 = [e["ts"] for e in ev if e["name"] == "deploy_start"][0]
+end = r.deploy_s * 1e6 + 300
+tids, agg, cnt = {}, collections.defaultdict(float), collections.Counter()
+for e in ev:
+    rel = e["ts"] - t0
+    if rel < 0 or rel > end:
+        continue
+    tid = tids.setdefault(e.get("tid"), len(tids))
+    d = e.get("dur", 0)
+    agg[e["name"]] += d
+    cnt[e["name"]] += 1
+    a = {k: v for k, v in (e.get("args") or {}).items() if k != "task"}
+    print("%7.2f +%6.2f t%d %-14s %s" % (rel / 1e3, d / 1e3, tid, e["name"], a))
+for k in agg:
+    print("  %-16s %3d %8.2f ms" % (k, cnt[k], agg[k] / 1e3))
+client.call("shutdown")
+proc.wait(10)
+for k in kids:
+    k.wait(10)

@@ -29,6 +29,18 @@ def _test_mode():
     yield
 
 
+@pytest.fixture(params=["mi355x", "reference"])
+def sched_profile(request):
+    """Runs a test under both scheduler flag profiles (``testing.profiles``): the defaults, and
+    every deviation from the reference switched off. Suites opt in with
+    ``pytestmark = pytest.mark.usefixtures("sched_profile")``."""
+    from dcos_commons_amd.testing import profiles
+
+    prev = profiles.use(request.param)
+    yield request.param
+    profiles.ACTIVE = prev
+
+
 def reference_path(*parts):
     p = os.path.join(REFERENCE, *parts)
     return p if os.path.exists(p) else None

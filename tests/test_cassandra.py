@@ -13,6 +13,9 @@ from dcos_commons_amd.testing import Expect, Send, ServiceTestRunner
 
 NODE_ENV = {"LOCAL_SEEDS": "foo,bar"}  # what Main injects into every pod
 
+# every test runs under the scheduler defaults and with every deviation from the reference off
+pytestmark = pytest.mark.usefixtures("sched_profile")
+
 
 def runner():
     return (ServiceTestRunner.for_framework("cassandra").set_pod_env("node", NODE_ENV)

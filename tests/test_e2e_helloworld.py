@@ -30,10 +30,17 @@ def hello_env(hello=2, world=2):
                 WORLD_READINESS_CHECK_TIMEOUT="10", GPU_PROBE_CMD="true")
 
 
+# every live-scheduler test runs under the scheduler defaults and with every deviation off
+pytestmark = pytest.mark.usefixtures("sched_profile")
+
+
 class Cluster:
     def __init__(self, spec_file="svc.yml", agents=3, gpus=0, env=None, transport="local", **cfg):
         self.env = env or hello_env()
         overrides = {"PORT_API": "0", "SDK_OFFER_WAIT_S": "0.5"}
+        from dcos_commons_amd.testing import profiles
+
+        overrides.update(profiles.ACTIVE)    # the suite's flag profile; the test's own flags win
         overrides.update(cfg)
         self.cfg = SchedulerConfig.for_testing(**overrides)
         raw = RawServiceSpec.new_builder(os.path.join(SPECS, spec_file)).set_env(self.env).build()
@@ -99,7 +106,10 @@ def test_helloworld_deploys_serially_and_reports_complete():
 
 
 def test_restart_and_replace_recover():
-    with Cluster() as c:
+    # the last check (stale reservations released while the scheduler goes idle) needs the MI355X
+    # reservation GC on every offer: the reference GCs only offers it leaves unused, and the offer
+    # carrying the replaced pod's reservations is the one its replacement launches on
+    with Cluster(SDK_RESERVATION_GC_ALL_OFFERS="true") as c:
         c.wait_plan("deploy")
         old = c.store.fetch_task("hello-0-server").task_id.value
         c.master.fail_task(old)

@@ -14,6 +14,9 @@ from dcos_commons_amd.scheduler.scheduler_config import SchedulerConfig
 from dcos_commons_amd.testing import Expect, Send, ServiceTestRunner
 from dcos_commons_amd.testing.cosmos import render_scheduler_environment
 
+# every test runs under the scheduler defaults and with every deviation from the reference off
+pytestmark = pytest.mark.usefixtures("sched_profile")
+
 ROOT = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "frameworks", "hdfs")
 
 

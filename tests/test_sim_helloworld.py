@@ -13,6 +13,9 @@ from dcos_commons_amd.testing import Expect, Send, ServiceTestRunner
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 SVC = os.path.join(ROOT, "frameworks", "helloworld", "specs", "svc.yml")
 
+# every test runs under the scheduler defaults and with every deviation from the reference off
+pytestmark = pytest.mark.usefixtures("sched_profile")
+
 ENV = dict(FRAMEWORK_NAME="hello-world", FRAMEWORK_PRINCIPAL="hello-world-principal", FRAMEWORK_USER="nobody",
            HELLO_COUNT="1", HELLO_PLACEMENT='[["hostname", "UNIQUE"]]', HELLO_CPUS="0.1", HELLO_MEM="252",
            HELLO_DISK="25", SLEEP_DURATION="1000", WORLD_COUNT="2", WORLD_PLACEMENT='[["hostname", "UNIQUE"]]',
@@ -124,7 +127,8 @@ def test_replace_pod_recycles_reservations_in_one_accept():
         Send.task_status("world-0-server", P.TASK_RUNNING).set_readiness_check_exit_code(0).build(),
         Expect.all_plans_complete(),
     ]
-    result = runner().run(ticks)
+    # the MI355X behaviour is SDK_RESERVATION_GC_ALL_OFFERS (off under the reference flags)
+    result = runner().set_scheduler_env(SDK_RESERVATION_GC_ALL_OFFERS="true").run(ticks)
     ops = [o.type for o in result.cluster_state.driver.accepts[-1].operations]
     Op = P.Offer.Operation
     assert ops.index(Op.UNRESERVE) < ops.index(Op.RESERVE) < ops.index(Op.LAUNCH_GROUP)
