@@ -1,0 +1,273 @@
+"""BASELINE configs 3 and 4 in cluster mode: cassandra deploy + seed-node replace, hdfs deploy +
+rolling configuration update, each service installed through Cosmos and run by Marathon as its
+own scheduler process (ZooKeeper persistence, Mesos v1 HTTP API) on the local DC/OS stand-in.
+
+``framework_bench`` runs the same scenarios with the scheduler, the master and an in-memory
+persister in one interpreter. Here every ZooKeeper write and Mesos call is a round trip between
+processes: a reference hdfs TaskInfo is 16-32 KB (its environment three times over) and the state
+store batches writes at 1 MB, so this is where those sizes cost. ``--specs reference`` installs the
+reference's unchanged packages (``testing.cluster.reference_packages``: its ``universe/`` and
+``src/main/dist``), ``--specs repo`` this repository's.
+
+* cassandra (3 nodes): deploy, timed from the master accepting SUBSCRIBE to ``/v1/plans/deploy``
+  answering 200; then ``POST /v1/pod/node-0/replace`` until the seed node's replacement is RUNNING
+  and ready and ``/v1/plans/recovery`` answers 200 (``CassandraRecoveryPlanOverrider`` restarts the
+  other two nodes too, so they learn the new seed address).
+* hdfs (3 journal, 2 name + zkfc, 3 data): deploy, timed the same way; then an ``hdfs-site.xml``
+  change (``TASKCFG_ALL_CLIENT_READ_SHORTCIRCUIT_STREAMS_CACHE_EXPIRY_MS`` + 1, the reference's
+  ``test_modify_app_config``; a package without that option gets its name-node handler count + 1): Marathon restarts the scheduler and its ``update`` plan relaunches
+  every node. ``update_s`` is timed from the new scheduler's SUBSCRIBE to the plan answering 200
+  with every node relaunched; ``update_total_s`` from the Marathon update (it includes starting the
+  scheduler process).
+
+Task payloads are synthetic (no Cassandra/HDFS binaries here): RUNNING at once, ONCE/FINISH tasks
+exit FINISHED at once, readiness checks pass at their first run. The hdfs journal and data nodes' first
+readiness checks are moved to 0 s through the package's own options (defaults: 30 s and 120 s).
+
+    python -m dcos_commons_amd.benchmarks.framework_cluster_bench --framework cassandra --specs reference
+"""
+from __future__ import annotations
+
+import argparse
+import http.client
+import json
+import logging
+import statistics
+import threading
+import time
+import urllib.parse
+from typing import Dict, List, Optional
+
+from dcos_commons_amd.mesos import protos as P
+
+FINISH_TASKS = ("-init_system_keyspaces", "-format", "-bootstrap", "-zkfc-format")
+HDFS_TASKS = 10
+HDFS_OPTIONS = {"journal_node": {"readiness_check": {"delay": 0, "interval": 1}},
+                "data_node": {"readiness_check": {"delay": 0, "interval": 1}}}
+APP_CONFIG_FIELDS = ("TASKCFG_ALL_CLIENT_READ_SHORTCIRCUIT_STREAMS_CACHE_EXPIRY_MS",   # the reference's test
+                     "TASKCFG_ALL_HDFS_NAME_NODE_HANDLER_COUNT")
+
+
+class _Watch:
+    """Master-side observations: every SUBSCRIBE per framework name, each task's last status."""
+
+    def __init__(self, cluster):
+        self.cond = threading.Condition()
+        self.subscribes: Dict[str, List[float]] = {}
+        self.statuses: Dict[str, P.TaskStatus] = {}
+        master = cluster.master
+        orig = master.subscribe
+
+        def subscribe(driver, info, _orig=orig):
+            with self.cond:
+                self.subscribes.setdefault(info.name, []).append(time.perf_counter())
+                self.cond.notify_all()
+            return _orig(driver, info)
+        master.subscribe = subscribe
+        master.add_status_listener(self._on_status)
+
+    def _on_status(self, framework_id: str, status: P.TaskStatus) -> None:
+        with self.cond:
+            self.statuses[status.task_id.value] = status
+            self.cond.notify_all()
+
+    def wait(self, pred, timeout_s: float, what: str) -> None:
+        deadline = time.monotonic() + timeout_s
+        with self.cond:
+            while not pred():
+                left = deadline - time.monotonic()
+                if left <= 0:
+                    raise TimeoutError(f"timed out waiting for {what}")
+                self.cond.wait(min(left, 0.05))
+
+
+def _ready(status: Optional[P.TaskStatus]) -> bool:
+    if status is None or status.state != P.TASK_RUNNING:
+        return False
+    if not status.HasField("check_status"):
+        return True
+    cmd = status.check_status.command
+    return cmd.HasField("exit_code") and cmd.exit_code == 0
+
+
+class FrameworkClusterBench:
+    def __init__(self, framework: str, specs: str = "reference", agents: int = 5,
+                 allocation_interval_s: float = 1.0, timeout_s: float = 180.0,
+                 profile_env: Optional[Dict[str, str]] = None):
+        from dcos_commons_amd.testing.cluster import LocalCluster, use
+        from dcos_commons_amd.testing.cluster.reference_packages import (reference_packages, reference_root,
+                                                                         stage_scheduler_artifacts)
+
+        self.framework = framework
+        self.specs = specs
+        self.timeout_s = timeout_s
+        packages = None
+        root = None
+        if specs == "reference":
+            root = reference_root()
+            if root is None:
+                raise SystemExit("--specs reference: no reference tree (SDK_REFERENCE_ROOT, /root/reference or "
+                                 "ref_inputs/)")
+            packages = reference_packages(root)
+        env = {"SDK_LOCK_WAIT_S": "1"}
+        env.update(profile_env or {})
+        self.cluster = LocalCluster(agents=agents, executor="synthetic", zk_process=True, packages=packages,
+                                    finish_tasks=FINISH_TASKS, finish_after_s=0.0,
+                                    allocation_interval_s=allocation_interval_s,
+                                    scheduler_env=env).start()
+        use(self.cluster)
+        if root is not None:
+            stage_scheduler_artifacts(self.cluster, root)
+        self.watch = _Watch(self.cluster)
+        self._seq = 0
+
+    def close(self) -> None:
+        self.cluster.shutdown()
+
+    # -- helpers ---------------------------------------------------------------------------
+    def _tasks(self, svc: str) -> Dict[str, str]:
+        """Task name -> current task id of the service's live tasks."""
+        out = {}
+        for t in self.cluster.tasks(svc):
+            out[t.name] = t.id
+        return out
+
+    def _wait_plan(self, base: str, plan: str) -> float:
+        deadline = time.monotonic() + self.timeout_s
+        u = urllib.parse.urlsplit(base)
+        conn = http.client.HTTPConnection(u.hostname, u.port, timeout=5)
+        try:
+            while time.monotonic() < deadline:
+                try:
+                    conn.request("GET", f"/v1/plans/{plan}")
+                    r = conn.getresponse()
+                    r.read()
+                    if r.status == 200:
+                        return time.perf_counter()
+                except (OSError, http.client.HTTPException):
+                    conn.close()
+                time.sleep(0.002)
+        finally:
+            conn.close()
+        raise TimeoutError(f"/v1/plans/{plan} never answered 200")
+
+    def _wait_idle(self, svc: str) -> None:
+        def idle():
+            return any(fw.info.name == svc and fw.suppressed and fw.connected
+                       for fw in list(self.cluster.master.frameworks.values()))
+        deadline = time.monotonic() + self.timeout_s
+        while not idle():
+            if time.monotonic() > deadline:
+                raise TimeoutError(f"{svc} never suppressed offers")
+            time.sleep(0.005)
+
+    def _subscribe_count(self, svc: str) -> int:
+        with self.watch.cond:
+            return len(self.watch.subscribes.get(svc, []))
+
+    # -- cycles ----------------------------------------------------------------------------
+    def run_cycle(self) -> Dict[str, float]:
+        self._seq += 1
+        return self._cassandra() if self.framework == "cassandra" else self._hdfs()
+
+    def _install(self, package: str, svc: str, count: int, options: dict) -> float:
+        from dcos_commons_amd.testing.sdk import sdk_install
+
+        before = self._subscribe_count(svc)
+        sdk_install.install(package, svc, count, additional_options=options, wait_for_deployment=False,
+                            wait_for_all_conditions=False)
+        self.watch.wait(lambda: self._subscribe_count(svc) > before, self.timeout_s, f"{svc} SUBSCRIBE")
+        t0 = self.watch.subscribes[svc][-1]
+        return self._wait_plan(self.cluster.marathon.scheduler_url(svc), "deploy") - t0
+
+    def _cassandra(self) -> Dict[str, float]:
+        from dcos_commons_amd.testing.sdk import sdk_install
+
+        svc = f"cassandra-bench-{self._seq}"
+        deploy = self._install("cassandra", svc, 3, {})
+        base = self.cluster.marathon.scheduler_url(svc)
+        self._wait_idle(svc)
+        old = self._tasks(svc)["node-0-server"]
+        t1 = time.perf_counter()
+        conn = http.client.HTTPConnection(*urllib.parse.urlsplit(base).netloc.split(":"), timeout=10)
+        conn.request("POST", "/v1/pod/node-0/replace")
+        if conn.getresponse().status != 200:
+            raise RuntimeError("pod replace was refused")
+        conn.close()
+
+        def replaced():
+            tid = self._tasks(svc).get("node-0-server")
+            return tid is not None and tid != old and _ready(self.watch.statuses.get(tid))
+        self.watch.wait(replaced, self.timeout_s, "node-0 replaced")
+        replace = self._wait_plan(base, "recovery") - t1
+        sdk_install.uninstall("cassandra", svc)
+        return {"deploy_s": deploy, "replace_s": replace}
+
+    def _hdfs(self) -> Dict[str, float]:
+        from dcos_commons_amd.testing.sdk import sdk_install, sdk_marathon
+
+        svc = f"hdfs-bench-{self._seq}"
+        deploy = self._install("hdfs", svc, HDFS_TASKS, HDFS_OPTIONS)
+        self._wait_idle(svc)
+        before = self._tasks(svc)
+        nodes = [n for n in before if n.endswith(("-node", "-zkfc"))]
+        subs = self._subscribe_count(svc)
+        cfg = sdk_marathon.get_config(svc)
+        field = next(f for f in APP_CONFIG_FIELDS if f in cfg["env"])     # an hdfs-site.xml setting
+        cfg["env"][field] = str(int(cfg["env"][field]) + 1)
+        t1 = time.perf_counter()
+        self.cluster.marathon.update_app(cfg, wait=False)
+        self.watch.wait(lambda: self._subscribe_count(svc) > subs, self.timeout_s, f"{svc} re-SUBSCRIBE")
+        t_sub = self.watch.subscribes[svc][-1]
+        base = self.cluster.marathon.scheduler_url(svc)
+
+        def rolled():
+            now = self._tasks(svc)
+            return all(now.get(n) not in (None, before[n]) and _ready(self.watch.statuses.get(now[n]))
+                       for n in nodes)
+        self.watch.wait(rolled, self.timeout_s, "every hdfs node relaunched")
+        t_done = self._wait_plan(base, "deploy")
+        sdk_install.uninstall("hdfs", svc)
+        return {"deploy_s": deploy, "update_s": t_done - t_sub, "update_total_s": t_done - t1}
+
+
+def main(argv: Optional[List[str]] = None) -> int:
+    from dcos_commons_amd.benchmarks.deploy_bench import PROFILES
+
+    ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
+    ap.add_argument("--framework", choices=["cassandra", "hdfs"], required=True)
+    ap.add_argument("--specs", choices=["reference", "repo"], default="reference")
+    ap.add_argument("--cycles", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--profile", choices=sorted(PROFILES), default="mi355x")
+    ap.add_argument("--allocation-interval", type=float, default=1.0)
+    ap.add_argument("--cluster-switch-interval-ms", type=float, default=0.5,
+                    help="interpreter switch interval of this process (master, agents, bench); 0: Python's 5 ms")
+    args = ap.parse_args(argv)
+    if args.cluster_switch_interval_ms > 0:
+        import sys
+
+        sys.setswitchinterval(args.cluster_switch_interval_ms / 1000.0)
+    logging.basicConfig(level=logging.ERROR)
+    bench = FrameworkClusterBench(args.framework, args.specs, allocation_interval_s=args.allocation_interval,
+                                  profile_env=dict(PROFILES[args.profile]))
+    try:
+        for _ in range(args.warmup):
+            bench.run_cycle()
+        cycles = [bench.run_cycle() for _ in range(args.cycles)]
+    finally:
+        bench.close()
+    out = {"bench": "framework_cluster", "framework": args.framework, "specs": args.specs, "cycles": args.cycles,
+           "profile": args.profile, "allocation_interval_s": args.allocation_interval,
+           "data": "scheduler process (started by Marathon from the package's app) + v1 HTTP API + ZooKeeper; "
+                   "synthetic task payloads"}
+    for key in cycles[0]:
+        vals = [c[key] for c in cycles]
+        out[key] = {"median": round(statistics.median(vals), 6), "min": round(min(vals), 6),
+                    "max": round(max(vals), 6)}
+    print(json.dumps(out), flush=True)
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())

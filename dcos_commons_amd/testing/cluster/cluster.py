@@ -150,7 +150,7 @@ class LocalCluster:
                  packages: Optional[Dict[str, str]] = None, scheduler_env: Optional[Dict[str, str]] = None,
                  finish_tasks: Sequence[str] = (), dcos_version: str = "1.13.0", keep_work_dir: bool = False,
                  mount_disks: Sequence[tuple] = (), dcos_security: bool = False, zk_process: bool = False,
-                 gpu_probe_service: bool = False, gpu_inventory=None):
+                 gpu_probe_service: bool = False, gpu_inventory=None, finish_after_s: float = 0.2):
         self.work_dir = os.path.abspath(work_dir or tempfile.mkdtemp(prefix="sdk-cluster-"))
         self._own_work_dir = work_dir is None and not keep_work_dir
         self.region = region
@@ -181,7 +181,8 @@ class LocalCluster:
                                                 secret_resolver=self.resolve_secret, resolver=self.resolve,
                                                 artifact_resolver=self.resolve_artifact, extra_env=task_env)
         elif executor == "synthetic":
-            self.behavior = _SyntheticBehavior(finish_tasks)
+            # finish_after_s: how long a synthetic ONCE/FINISH task runs before it exits 0
+            self.behavior = _SyntheticBehavior(finish_tasks, finish_after_s)
         else:
             raise ValueError(f"executor must be 'process' or 'synthetic', not {executor!r}")
         self.executor = executor

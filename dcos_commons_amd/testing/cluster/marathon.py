@@ -356,6 +356,7 @@ class LocalMarathon:
         os.makedirs(sandbox, exist_ok=True)
         task = MarathonTask(tid, app.id, self._place(app), [app.api_port], sandbox, time.time())
         env = self._environment(app, task)
+        self._fetch(app.definition.get("fetch") or [], sandbox)
         cmd = app.definition.get("cmd") or ""
         with open(os.path.join(sandbox, "stdout"), "ab") as out, open(os.path.join(sandbox, "stderr"), "ab") as err:
             proc = subprocess.Popen(["bash", "-c", cmd], cwd=sandbox, env=env, stdin=subprocess.DEVNULL,
@@ -365,6 +366,40 @@ class LocalMarathon:
             app.running_version = app.version
             app.history.append(task)
         LOGGER.info("Marathon started %s (%s, pid %d, api port %d)", app.id, tid, proc.pid, app.api_port)
+
+    def _fetch(self, fetch: list, sandbox: str) -> None:
+        """The app's ``fetch`` URIs, as the Mesos fetcher stages them into the scheduler's sandbox,
+        from the cluster's artifact store (no network): a directory artifact stands for an
+        extracted archive and its contents are copied in; a file is copied, and extracted when it
+        is an archive and ``extract`` is not false. URIs the store does not hold (a JRE, the
+        libmesos bundle: nothing this SDK's schedulers run) are skipped."""
+        import shutil
+        import urllib.parse
+
+        for entry in fetch:
+            uri = entry.get("uri", "") if isinstance(entry, dict) else str(entry)
+            local = self.cluster.resolve_artifact(uri) if uri else None
+            if local is None:
+                LOGGER.info("marathon fetcher: skipping %s (not in the local artifact store)", uri)
+                continue
+            if os.path.isdir(local):
+                for name in os.listdir(local):
+                    src = os.path.join(local, name)
+                    if os.path.isdir(src):
+                        shutil.copytree(src, os.path.join(sandbox, name), dirs_exist_ok=True)
+                    else:
+                        shutil.copy2(src, os.path.join(sandbox, name))
+                continue
+            dest = os.path.join(sandbox, os.path.basename(urllib.parse.urlparse(uri).path) or "download")
+            shutil.copy2(local, dest)
+            if isinstance(entry, dict) and entry.get("executable"):
+                os.chmod(dest, 0o755)
+            elif (not isinstance(entry, dict) or entry.get("extract", True)) and \
+                    dest.endswith((".zip", ".tar.gz", ".tgz", ".tar")):
+                try:
+                    shutil.unpack_archive(dest, sandbox)
+                except (shutil.ReadError, ValueError, OSError) as e:
+                    LOGGER.warning("marathon fetcher: cannot extract %s: %s", dest, e)
 
     def _place(self, app: _App) -> str:
         """The agent the scheduler task runs on. Without app ``constraints`` that is the loopback
@@ -420,6 +455,12 @@ class LocalMarathon:
                     break
                 time.sleep(0.05)
             rc = proc.wait()
+            # the task's command ended: as the Mesos executor destroys the task's container,
+            # whatever it left running in its session (the scheduler under a killed shell) goes too
+            try:
+                os.killpg(proc.pid, signal.SIGKILL)
+            except (ProcessLookupError, PermissionError):
+                pass
             with app.lock:
                 if app.task is not None:
                     app.task.state = "TASK_KILLED" if (app.stopping or app.destroyed) else \

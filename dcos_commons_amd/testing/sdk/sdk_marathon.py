@@ -20,9 +20,11 @@ def app_exists(app_name: str) -> bool:
 
 
 def get_config(app_name: str) -> Dict[str, Any]:
-    """The app definition without runtime-only fields, ready for ``update_app``."""
+    """The app definition without runtime-only fields, ready for ``update_app``. ``fetch`` stays (as in
+    the reference's ``testing/sdk_marathon.py:40-52``): a package's scheduler is fetched on every
+    restart."""
     app = copy.deepcopy(_marathon().get_app(app_name))
-    for k in ("tasks", "tasksRunning", "deployments", "version", "uris", "lastTaskFailure", "fetch"):
+    for k in ("tasks", "tasksRunning", "deployments", "version", "uris", "lastTaskFailure"):
         app.pop(k, None)
     return app
 
