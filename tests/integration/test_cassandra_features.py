@@ -46,7 +46,7 @@ def _rendered(node, config):
     ``CONFIG_TEMPLATE_<name>``, rendered against the task's environment."""
     info = _server_info(node)
     env = {v["name"]: v.get("value", "") for v in info["command"]["environment"]["variables"]}
-    sandbox_path = env[f"CONFIG_TEMPLATE_{config.upper()}"].split(",")[0]   # "<fetched template>,<dest>"
+    sandbox_path = env[f"CONFIG_TEMPLATE_{config.upper().replace('-', '_')}"].split(",")[0]   # "<fetched template>,<dest>"
     url = next(u["value"] for u in info["command"]["uris"] if u.get("outputFile") == sandbox_path)
     template = sdk_cmd.service_request("GET", SVC, urllib.parse.urlparse(url).path, retry=False).text
     return render_mustache(config, template, env, [])
@@ -183,5 +183,41 @@ def test_authentication_settings():
     try:
         cfg = _rendered(0, "cassandra")
         assert "authenticator: PasswordAuthenticator" in cfg
+    finally:
+        sdk_install.uninstall(PACKAGE, SVC)
+
+
+def test_secure_jmx_g1_and_metrics_toggle():
+    """Secure JMX (its credentials from the cluster's secret store), the G1 collector and the
+    metrics reporter, set at install and then changed by a package update that rolls every node."""
+    c = sdk_install._cluster()
+    for name, data in (("jmx/password", b"admin secret\n"), ("jmx/access", b"admin readwrite\n"),
+                       ("jmx/keystore", b"KS"), ("jmx/keystore-pass", b"changeit\n")):
+        c.secrets[f"{SVC.strip('/')}/{name}"] = data
+    jmx = {"enabled": True, "password_file": f"{SVC.strip('/')}/jmx/password",
+           "access_file": f"{SVC.strip('/')}/jmx/access", "key_store": f"{SVC.strip('/')}/jmx/keystore",
+           "key_store_password_file": f"{SVC.strip('/')}/jmx/keystore-pass"}
+    sdk_install.install(PACKAGE, SVC, 3, additional_options={"service": {"jmx": jmx},
+                                                             "nodes": {"heap": {"gc": "G1"}}})
+    try:
+        for i in range(3):
+            info = _server_info(i)
+            secret_files = sorted(v["containerPath"] for v in info.get("container", {}).get("volumes", [])
+                                  if v.get("source", {}).get("type") == "SECRET")
+            assert secret_files == ["jmx/access_file", "jmx/key_store", "jmx/key_store_password_file",
+                                    "jmx/password_file"], secret_files
+            assert "bash ./jmx-ssl-setup.sh" in info["command"]["value"]
+            assert "metricsReporterConfigFile" in info["command"]["value"]
+        assert "-XX:+UseG1GC" in _rendered(0, "jvm")
+        assert "rmi.port=7198" in _rendered(0, "jmx-ssl-setup")
+
+        ids = sdk_tasks.get_task_ids(SVC, "node")
+        sdk_upgrade.update_or_upgrade_or_downgrade(
+            PACKAGE, SVC, to_version=None, expected_running_tasks=3,
+            to_options={"cassandra": {"metrics_enabled": False}, "nodes": {"heap": {"gc": "CMS"}}})
+        sdk_tasks.check_tasks_updated(SVC, "node", ids)
+        sdk_plan.wait_for_completed_deployment(SVC)
+        assert "metricsReporterConfigFile" not in _server_info(0)["command"]["value"]
+        assert "-XX:+UseConcMarkSweepGC" in _rendered(0, "jvm")
     finally:
         sdk_install.uninstall(PACKAGE, SVC)

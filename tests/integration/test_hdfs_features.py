@@ -104,3 +104,30 @@ def test_upgrade_and_downgrade():
         sdk_plan.wait_for_completed_deployment(SVC)
     finally:
         sdk_install.uninstall(PACKAGE, SVC)
+
+
+def test_kerberos_tls_and_metrics_together():
+    """Kerberos (keytab from the secret store, krb5.conf), HTTPS (ssl-server/ssl-client from the
+    provisioned TLS artifacts) and the metrics2 StatsD sinks, all on: every node gets the templates
+    and the flags that use them."""
+    c = sdk_install._cluster()
+    c.secrets["__dcos_base64__hdfs_keytab"] = b"not-a-real-keytab"
+    sdk_install.install(PACKAGE, SVC, DEFAULT_TASK_COUNT, additional_options=_opts({
+        "service": {"service_account": ACCOUNT, "service_account_secret": ACCOUNT_SECRET,
+                    "security": {"transport_encryption": {"enabled": True},
+                                 "kerberos": {"enabled": True, "realm": "EXAMPLE.COM",
+                                              "kdc": {"hostname": "kdc.example.com", "port": 88}}}},
+        "hdfs": {"metrics_enabled": True}}))
+    try:
+        for task in ("journal-0-node", "name-0-node", "name-1-node", "data-0-node"):
+            info = _info(task)
+            env = {v["name"]: v.get("value", "") for v in info["command"]["environment"]["variables"]}
+            for cfg in ("KRB5", "SSL_SERVER", "SSL_CLIENT", "HADOOP_METRICS2"):
+                assert f"CONFIG_TEMPLATE_{cfg}" in env, (task, cfg)
+            assert env["SECURITY_KERBEROS_KDC_HOSTNAME"] == "kdc.example.com"
+            assert env["SECURITY_KERBEROS_REALM"] == "EXAMPLE.COM"
+            assert "-Djava.security.krb5.conf=" in info["command"]["value"]
+        site = sdk_networks.get_endpoint_string(PACKAGE, SVC, "hdfs-site.xml")
+        assert "HTTPS_ONLY" in site and "ssl-server.xml" in site
+    finally:
+        sdk_install.uninstall(PACKAGE, SVC)

@@ -117,7 +117,7 @@ def test_launch_task_with_multiple_ports():
             "Unable to find matching task"
         info = sdk_cmd.service_request("GET", config.SERVICE_NAME, "/v1/pod/multiport-0/info").json()[0]["info"]
         ports = {p["name"]: p["number"] for p in info["discovery"]["ports"]["ports"]}
-        assert ports["static"] == 4444 and 7000 <= ports["ranged"] <= 7100
+        assert ports["static"] == 1729 and 7000 <= ports["ranged"] <= 7100     # the package's hello.port_one
         assert len(set(ports.values())) == 5, ports
         # every port is reserved for the task: the agent's port ranges cover them
         ranges = [(int(r["begin"]), int(r["end"])) for res in info["resources"] if res["name"] == "ports"

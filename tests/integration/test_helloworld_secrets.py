@@ -143,10 +143,28 @@ def _executor_container(pod):
 
 
 def test_seccomp():
-    sdk_install.install(config.PACKAGE_NAME, config.SERVICE_NAME, 1, additional_options={"service": {"yaml": "seccomp"}})
+    sdk_install.install(config.PACKAGE_NAME, config.SERVICE_NAME, 1, additional_options={"service": {"yaml": "seccomp"},
+                                                                        "hello": {"seccomp-unconfined": True}})
     try:
         task = sdk_cmd.service_request("GET", config.SERVICE_NAME, "/v1/pod/hello-0/info").json()[0]["info"]
         assert task["container"]["linuxInfo"]["seccomp"]["unconfined"] is True
+    finally:
+        sdk_install.uninstall(config.PACKAGE_NAME, config.SERVICE_NAME)
+
+
+def test_custom_seccomp_profile():
+    """Reference test_seccomp.py: install with a named agent profile, then switch the profile
+    through the scheduler's Marathon env; the pods roll to the new profile."""
+    sdk_install.install(config.PACKAGE_NAME, config.SERVICE_NAME, 1,
+                        additional_options={"service": {"yaml": "seccomp"}, "hello": {"seccomp-profile-name": "default.json"}})
+    try:
+        info = lambda: sdk_cmd.service_request("GET", config.SERVICE_NAME, "/v1/pod/hello-0/info").json()[0]["info"]
+        assert info()["container"]["linuxInfo"]["seccomp"]["profileName"] == "default.json"
+        app = sdk_marathon.get_config(config.SERVICE_NAME)
+        app["env"]["HELLO_SECCOMP_PROFILE_NAME"] = "test_profile.json"
+        sdk_marathon.update_app(app)
+        sdk_plan.wait_for_completed_deployment(config.SERVICE_NAME)
+        assert info()["container"]["linuxInfo"]["seccomp"]["profileName"] == "test_profile.json"
     finally:
         sdk_install.uninstall(config.PACKAGE_NAME, config.SERVICE_NAME)
 

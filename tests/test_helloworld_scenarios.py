@@ -96,7 +96,12 @@ def test_container_features():
 
     def seccomp(sim):  # seccomp applies to the task container (PodInfoBuilder.java:592-605)
         assert _launched(sim)["hello-0-server"].container.linux_info.seccomp.unconfined
-    _run("seccomp.yml", seccomp)
+    _run("seccomp.yml", seccomp, env={"HELLO_SECCOMP_UNCONFINED": "true"})
+
+    def profile(sim):
+        seccomp = _launched(sim)["hello-0-server"].container.linux_info.seccomp
+        assert not seccomp.unconfined and seccomp.profile_name == "default.json"
+    _run("seccomp.yml", profile, env={"HELLO_SECCOMP_PROFILE_NAME": "default.json"})
 
     def host_vol(sim):
         vols = {v.container_path: v for v in _launched(sim)["hello-0-server"].container.volumes}

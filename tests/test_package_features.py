@@ -1,0 +1,205 @@
+"""Every shipped cassandra and hdfs config template, rendered with the optional features on:
+TLS (transport encryption), Kerberos, metrics reporting, the G1 collector, secure JMX.
+
+The harness renders every config file of every task of pod 0 strictly (a value the task
+environment lacks fails the run), so each case below also proves the templates it turns on
+render; the assertions check what the application will read."""
+import os
+import subprocess
+import xml.etree.ElementTree as ET
+
+import pytest
+
+from dcos_commons_amd.testing import ServiceTestRunner
+from dcos_commons_amd.testing.cosmos import render_marathon_app
+
+import test_cassandra
+import test_hdfs
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+CRED = '{"uid": "svc", "private_key": "k"}'
+
+
+def _props(xml: str) -> dict:
+    return {p.findtext("name"): p.findtext("value") for p in ET.fromstring(xml).iter("property")}
+
+
+# -- cassandra -----------------------------------------------------------------------------------
+def test_cassandra_defaults_render_cms_metrics_and_cqlsh():
+    r = test_cassandra.runner().run()
+    jvm = r.get_task_config("node", "server", "jvm")
+    assert "-XX:+UseConcMarkSweepGC" in jvm and "-Xmx" in jvm and "-Xmn" in jvm and "PrintGCDetails" not in jvm
+    metrics = r.get_task_config("node", "server", "metrics-reporter")
+    assert "statsd:" in metrics and "port: 99999" in metrics        # the task's STATSD_UDP_PORT
+    cqlshrc = r.get_task_config("node", "server", "cqlshrc")
+    assert "port = 9042" in cqlshrc and "[ssl]" not in cqlshrc
+    server = r.service_spec.pod("node").task("server")
+    assert "metricsReporterConfigFile" in server.command.value and "jmx-ssl-setup" not in server.command.value
+    assert not r.service_spec.pod("node").secrets
+
+
+def test_cassandra_g1_with_gc_logging():
+    r = test_cassandra.runner().set_options("nodes.heap.gc", "G1", "nodes.heap.gc_logging", "true",
+                                            "nodes.heap.g1_max_pause_ms", "300").run()
+    jvm = r.get_task_config("node", "server", "jvm")
+    assert "-XX:+UseG1GC" in jvm and "-XX:MaxGCPauseMillis=300" in jvm and "ConcMarkSweep" not in jvm
+    assert "-Xmn" not in jvm and "-Xloggc:" in jvm
+    jvm_spec = next(c for c in r.service_spec.pod("node").task("server").config_files if c.name == "jvm")
+    with open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "frameworks", "cassandra",
+                           "specs", "jvm_G1.options"), encoding="utf-8") as f:
+        assert jvm_spec.template_content == f.read()
+
+
+def test_cassandra_tls_cqlsh_and_metrics_off():
+    r = (test_cassandra.runner().set_options("service.security.transport_encryption.enabled", "true",
+                                             "cassandra.metrics_enabled", "false")
+         .set_scheduler_env(DCOS_SERVICE_ACCOUNT_CREDENTIAL=CRED).run())
+    cqlshrc = r.get_task_config("node", "server", "cqlshrc")
+    assert "[ssl]" in cqlshrc and "node.ca" in cqlshrc and "ssl_transport_factory" in cqlshrc
+    assert "metricsReporterConfigFile" not in r.service_spec.pod("node").task("server").command.value
+
+
+def test_cassandra_secure_jmx(tmp_path):
+    r = (test_cassandra.runner()
+         .set_options("service.jmx.enabled", "true", "service.jmx.password_file", "cassandra/jmx-pw",
+                      "service.jmx.access_file", "cassandra/jmx-access", "service.jmx.key_store", "cassandra/ks",
+                      "service.jmx.key_store_password_file", "cassandra/ks-pw",
+                      "service.jmx.add_trust_store", "true", "service.jmx.trust_store", "cassandra/ts",
+                      "service.jmx.trust_store_password_file", "cassandra/ts-pw").run())
+    pod = r.service_spec.pod("node")
+    files = sorted(s.file_path for s in pod.secrets)
+    assert files == ["jmx/access_file", "jmx/key_store", "jmx/key_store_password_file", "jmx/password_file",
+                     "jmx/trust_store", "jmx/trust_store_password_file"]
+    server = pod.task("server")
+    assert "bash ./jmx-ssl-setup.sh" in server.command.value and "LOCAL_JMX=no" in server.command.value
+    ports = {p.port_name: p for p in server.resource_set.resources if getattr(p, "port_name", "")}
+    assert "jmx-rmi" in ports and "7198" in str(ports["jmx-rmi"].value)
+    # the rendered setup script, run in a sandbox holding the secrets, writes the JVM flags
+    script = r.get_task_config("node", "server", "jmx-ssl-setup")
+    sandbox = tmp_path / "sandbox"
+    (sandbox / "jmx").mkdir(parents=True)
+    for name, text in (("password_file", "admin secret\n"), ("access_file", "admin readwrite\n"),
+                       ("key_store", "KS"), ("key_store_password_file", "kspass\n"), ("trust_store", "TS"),
+                       ("trust_store_password_file", "tspass\n")):
+        (sandbox / "jmx" / name).write_text(text)
+    (sandbox / "jmx-ssl-setup.sh").write_text(script)
+    p = subprocess.run(["bash", "jmx-ssl-setup.sh"], cwd=sandbox, env=dict(os.environ, MESOS_SANDBOX=str(sandbox)),
+                       capture_output=True, text=True, timeout=30)
+    assert p.returncode == 0, p.stderr
+    opts = (sandbox / "jmx.options").read_text()
+    assert "-Dcom.sun.management.jmxremote.port=7199" in opts and "rmi.port=7198" in opts
+    assert "keyStorePassword=kspass" in opts and "trustStorePassword=tspass" in opts
+    assert oct((sandbox / "jmx" / "password_file").stat().st_mode & 0o777) == "0o400"
+    # a missing secret stops the task before Cassandra starts
+    (sandbox / "jmx" / "access_file").unlink()
+    assert subprocess.run(["bash", "jmx-ssl-setup.sh"], cwd=sandbox, env=dict(os.environ, MESOS_SANDBOX=str(sandbox)),
+                          capture_output=True, text=True, timeout=30).returncode == 1
+
+
+# -- hdfs ----------------------------------------------------------------------------------------
+def _hdfs(**options):
+    r = test_hdfs.runner()
+    flat = [x for kv in options.items() for x in kv]
+    return r.set_options(*flat).set_scheduler_env(DCOS_SERVICE_ACCOUNT_CREDENTIAL=CRED).run()
+
+
+def test_hdfs_metrics2_per_role():
+    r = test_hdfs.runner().run()
+    for pod, prefix in (("journal", "journalnode"), ("name", "namenode"), ("data", "datanode")):
+        m = r.get_task_config(pod, "node", "hadoop-metrics2")
+        assert f"{prefix}.sink.statsd.class=org.apache.hadoop.metrics2.sink.StatsDSink" in m
+        assert f"{prefix}.sink.statsd.server.port=99999" in m and f"service.name={pod}-0" in m
+    off = test_hdfs.runner().set_options("hdfs.metrics_enabled", "false").run()
+    assert "sink.statsd" not in off.get_task_config("data", "node", "hadoop-metrics2")
+
+
+def test_hdfs_https_with_tls():
+    r = _hdfs(**{"service.security.transport_encryption.enabled": "true",
+                 "service.security.transport_encryption.excluded_ciphers": "TLS_RSA_WITH_RC4_128_MD5"})
+    for pod in ("journal", "name", "data"):
+        site = _props(r.get_task_config(pod, "node", "hdfs-site"))
+        assert site["dfs.http.policy"] == "HTTPS_ONLY"
+        assert site["dfs.https.server.keystore.resource"] == "ssl-server.xml"
+        server = _props(r.get_task_config(pod, "node", "ssl-server"))
+        assert server["ssl.server.keystore.location"].endswith("/node.keystore")
+        assert server["ssl.server.exclude.cipher.list"] == "TLS_RSA_WITH_RC4_128_MD5"
+        client = _props(r.get_task_config(pod, "node", "ssl-client"))
+        assert client["ssl.client.truststore.location"].endswith("/node.truststore")
+    names = {c.name for c in r.service_spec.pod("name").task("zkfc").config_files}
+    assert "ssl-client" in names and "ssl-server" not in names
+
+
+def test_hdfs_kerberos_krb5_conf_and_jvm_flag():
+    r = _hdfs(**{"service.security.kerberos.enabled": "true", "service.security.kerberos.realm": "EXAMPLE.COM",
+                 "service.security.kerberos.kdc.hostname": "kdc.example.com",
+                 "service.security.kerberos.kdc.port": "88"})
+    krb5 = r.get_task_config("name", "node", "krb5")
+    assert "default_realm = EXAMPLE.COM" in krb5 and "kdc = kdc.example.com:88" in krb5
+    assert "udp_preference_limit = 1" in krb5
+    for pod in ("journal", "name", "data"):
+        cmd = r.service_spec.pod(pod).task("node").command.value
+        assert "-Djava.security.krb5.conf=" in cmd and "./keytab-fix" in cmd
+        assert "hadoop.security.authentication" in r.get_task_config(pod, "node", "core-site")
+    assert {c.name for c in r.service_spec.pod("name").task("format").config_files} >= {"krb5"}
+
+
+def test_hdfs_everything_on():
+    """TLS, Kerberos and metrics together: every template of every pod renders."""
+    r = _hdfs(**{"service.security.transport_encryption.enabled": "true",
+                 "service.security.kerberos.enabled": "true", "hdfs.metrics_enabled": "true"})
+    for pod in ("journal", "name", "data"):
+        names = {c.name for c in r.service_spec.pod(pod).task("node").config_files}
+        assert names == {"core-site", "hdfs-site", "hadoop-metrics2", "ssl-server", "ssl-client", "krb5"}
+        for name in names:
+            assert r.get_task_config(pod, "node", name)
+
+
+# -- helloworld ----------------------------------------------------------------------------------
+def _hello(spec="svc.yml"):
+    return ServiceTestRunner.for_framework("helloworld", spec).set_scheduler_env(SDK_REVIVE_INTERVAL_S="0")
+
+
+def test_helloworld_rlimits_and_labels():
+    """hello.rlimits / world.rlimits (default 128000 open files, like the reference package) and
+    hello.labels reach the pods and the hello task."""
+    r = _hello().run()
+    for pod in ("hello", "world"):
+        (rl,) = r.service_spec.pod(pod).rlimits
+        assert (rl.name, rl.soft, rl.hard) == ("RLIMIT_NOFILE", 128000, 128000)
+    assert not r.service_spec.pod("hello").task("server").labels
+    r = _hello().set_options("hello.labels", "team:infra,tier:gold",
+                             "world.rlimits.rlimit_nofile.soft", "4096").run()
+    assert r.service_spec.pod("hello").task("server").labels == {"team": "infra", "tier": "gold"}
+    assert r.service_spec.pod("world").rlimits[0].soft == 4096
+
+
+def test_helloworld_scenario_options():
+    """port_one (multiport), seccomp-* (seccomp), volume_profile (profile-mount-volume)."""
+    r = _hello("multiport.yml").set_options("hello.port_one", "4321").run()
+    ports = {p.port_name: p for p in r.service_spec.pod("multiport").task("server").resource_set.resources
+             if getattr(p, "port_name", "")}
+    assert "4321" in str(ports["static"].value)
+    pod = _hello("seccomp.yml").run().service_spec.pod("hello")
+    assert not pod.seccomp_unconfined and pod.seccomp_profile_name is None
+    pod = _hello("seccomp.yml").set_options("hello.seccomp-unconfined", "true").run().service_spec.pod("hello")
+    assert pod.seccomp_unconfined
+    pod = _hello("seccomp.yml").set_options("hello.seccomp-profile-name", "default.json").run().service_spec.pod("hello")
+    assert not pod.seccomp_unconfined and pod.seccomp_profile_name == "default.json"
+    for profile, expect in (("", "fast-nvme"), ("xfs", "xfs")):
+        r = _hello("profile-mount-volume.yml").set_options("hello.volume_profile", profile).run()
+        text = repr(r.service_spec.pod("hello").to_dict() if hasattr(r.service_spec.pod("hello"), "to_dict")
+                    else r.service_spec.pod("hello"))
+        assert expect in text
+
+
+def test_helloworld_marathon_health_check_and_env():
+    app = render_marathon_app(os.path.join(ROOT, "frameworks", "helloworld", "universe"),
+                              {"service.check.intervalSeconds": "30", "service.verbose_mesos_logging": "0"})
+    (hc,) = app["healthChecks"]
+    assert hc["path"] == "/v1/health" and hc["intervalSeconds"] == 30 and hc["timeoutSeconds"] == 20
+    assert hc["delaySeconds"] == 15
+    env = app["env"]
+    assert env["GLOG_v"] == "0" and env["HELLO_PORT_ONE"] == "1729" and env["HELLO_SECCOMP_UNCONFINED"] == "false"
+    assert "HELLO_SECCOMP_PROFILE_NAME" not in env and "HELLO_VOLUME_PROFILE" not in env
+    assert env["KEYSTORE_APP_VERSION"] and env["NGINX_CONTAINER_VERSION"]

@@ -253,3 +253,48 @@ def test_master_with_agent_runtimes_reports_what_its_own_lifecycle_would():
         return seen
     assert run(True) == run(False) == [("TASK_STARTING", None, ["0"]), ("TASK_RUNNING", None, ["0"]),
                                        ("TASK_RUNNING", 0, ["0"])]
+
+
+@pytest.mark.gpu
+def test_agent_runtime_gates_readiness_on_the_hip_probe():
+    """The split topology's agent side on an MI355X: every pod's readiness check runs the fused HIP
+    probe (``ops.readiness``) on the agent's device, from the agent's runtime; the scheduler gets
+    the result over the framed stream."""
+    from dcos_commons_amd import ops
+    from dcos_commons_amd.benchmarks import deploy_bench as DB
+    from dcos_commons_amd.benchmarks.runner import gpu_check_runner
+
+    probe = gpu_check_runner()
+    ran = []
+
+    def check(devices):
+        ran.append(list(devices))
+        return probe(None, devices)
+    master, links = _runtime_master(2, check=check)
+    # both agents own device 0 of this box (their AgentSpec names device i; map them onto 0)
+    for link in links:
+        link.runtime._check = lambda devices: check([0])
+    stream = StreamMaster(master).start()
+
+    class Cluster:
+        def driver(self, sched, info):
+            return StreamSchedulerDriver(stream.address, sched, info)
+
+        def placement(self):
+            return master.placement()
+
+        def fail_task(self, tid):
+            master.fail_task(tid)
+
+        def shutdown(self):
+            pass
+
+    bench = DB.DeployBench(2, timeout_s=60, allocation_interval_s=0.05)
+    bench._make_master = lambda: Cluster()
+    try:
+        r = bench.run_cycle()
+        assert r.deploy_s > 0 and len(ran) >= 4 and all(d == [0] for d in ran)
+        assert ops.lib() is not None        # the in-tree HIP extension served the checks
+    finally:
+        stream.stop()
+        master.shutdown()
