@@ -44,7 +44,8 @@ PROFILES = {
                   "SDK_RESERVATION_GC_ALL_OFFERS": "false",
                   "SDK_FAST_UNSUPPRESS": "false", "SDK_MERGE_AGENT_OFFERS": "false",
                   "SDK_LAUNCH_RECONCILE_S": "0", "SDK_UNKNOWN_AS_LOST": "false", "SDK_STREAM_LAUNCHES": "false",
-                  "SDK_REVIVE_ONLY_UNMATCHED": "false", "SDK_GC_GEN0_THRESHOLD": "0"},
+                  "SDK_REVIVE_ONLY_UNMATCHED": "false", "SDK_GC_GEN0_THRESHOLD": "0",
+                  "SDK_STATUS_CYCLE_WAIT_MS": "0"},
 }
 
 

@@ -52,6 +52,7 @@ class FrameworkScheduler:
     def __init__(self, roles_whitelist, scheduler_config, persister, framework_store, client,
                  offer_processor: OfferProcessor = None, implicit_reconciler: ImplicitReconciler = None):
         self.roles_whitelist = set(roles_whitelist)
+        self.status_cycle_wait_s = scheduler_config.status_cycle_wait_s() if scheduler_config is not None else 0.0
         self.framework_store = framework_store
         self.client = client
         self.offer_processor = offer_processor or OfferProcessor(
@@ -100,8 +101,20 @@ class FrameworkScheduler:
         if master_info is not None and master_info.HasField("domain"):
             IsLocalRegionRule.set_local_domain(master_info.domain)
 
+    def _gate_statuses(self, driver) -> None:
+        """Network drivers call the status callbacks from their own reader thread, which holds
+        no lock of the scheduler's: there a status may wait for a running offer cycle
+        (``OfferProcessor.wait_cycle_idle``). In-process masters deliver from their own threads
+        and get no gate."""
+        wait_s = self.status_cycle_wait_s
+        set_gate = getattr(driver, "set_status_gate", None)
+        if set_gate is not None and wait_s > 0:
+            processor = self.offer_processor
+            set_gate(lambda: processor.wait_cycle_idle(wait_s))
+
     # -- Mesos callbacks ---------------------------------------------------------------
     def registered(self, driver, framework_id: P.FrameworkID, master_info) -> None:
+        trace.instant("registered", "driver")
         try:
             with self._lock:
                 again = self._register_called
@@ -115,6 +128,7 @@ class FrameworkScheduler:
                 LOGGER.error("Unable to store registered framework ID '%s'", framework_id.value)
                 ProcessExit.exit(ProcessExit.REGISTRATION_FAILURE, e)
             self._update_driver_and_domain(driver, master_info)
+            self._gate_statuses(driver)
             self.client.registered(False)
             self.offer_processor.start()
             self.implicit_reconciler.start()
@@ -124,11 +138,13 @@ class FrameworkScheduler:
     def reregistered(self, driver, master_info) -> None:
         try:
             self._update_driver_and_domain(driver, master_info)
+            self._gate_statuses(driver)
             self.client.registered(True)
         except Exception as e:  # noqa: BLE001
             self._exit(e)
 
     def resource_offers(self, driver, offers) -> None:
+        trace.instant("offers_in", "driver", n=len(offers))
         try:
             metrics.increment_received_offers(len(offers))
             if not self._api_server_started.is_set():

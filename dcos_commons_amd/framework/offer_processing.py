@@ -482,6 +482,10 @@ class OfferProcessor:
         self._stop = threading.Event()
         self._thread: Optional[threading.Thread] = None
         self.cycles = 0
+        # set while a cycle evaluates offers; status callbacks of a network driver wait for it to
+        # clear (``wait_cycle_idle``) rather than take the interpreter lock from the cycle
+        self._cycle_cv = threading.Condition()
+        self._cycle_active = False
 
     def disable_threading(self) -> "OfferProcessor":
         self.multithreaded = False
@@ -608,7 +612,14 @@ class OfferProcessor:
             with metrics.process_offers_timer(), trace.span("offer_cycle", "offers", new=len(new_offers),
                                                                held=len(held)) as sp:
                 if self._check_status():
-                    self._evaluate(offers, now)
+                    with self._cycle_cv:
+                        self._cycle_active = True
+                    try:
+                        self._evaluate(offers, now)
+                    finally:
+                        with self._cycle_cv:
+                            self._cycle_active = False
+                            self._cycle_cv.notify_all()
                     sp.set(working=True)
                     if self.revive_only_unmatched and self.revive_manager.revive_requested and \
                             self._candidates_all_launched():
@@ -649,6 +660,20 @@ class OfferProcessor:
             with self._in_progress_lock:
                 for o in new_offers:
                     self._in_progress.discard(o.id.value)
+
+    def wait_cycle_idle(self, timeout_s: float) -> None:
+        """Blocks while an offer cycle is evaluating, for at most ``timeout_s``.
+
+        The scheduler's threads share one interpreter lock. A status batch handled while a cycle
+        runs takes that lock whenever the cycle releases it (every ACCEPT written to the master
+        socket releases it), and the cycle then waits for the whole batch: on the MI355X box an
+        8-pod cycle ran 7.2 ms of wall time for 4.9 ms of its own CPU, the rest spent behind the
+        first pods' STARTING/RUNNING updates (profiles/split_timeline_n8_r06_box.txt). Nothing in
+        a cycle waits for a status, so the statuses that queue up meanwhile are handled in one
+        batch when it ends, and the last pod's launch leaves that much earlier."""
+        with self._cycle_cv:
+            if self._cycle_active:
+                self._cycle_cv.wait_for(lambda: not self._cycle_active, timeout_s)
 
     def _reoffer_revive(self) -> bool:
         self.revive_manager.request_revive(bypass_spacing=True)

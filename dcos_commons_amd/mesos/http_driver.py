@@ -35,7 +35,7 @@ import socket
 import threading
 import time
 import urllib.parse
-from typing import Iterable, List, Optional
+from typing import Callable, Iterable, List, Optional
 
 from dcos_commons_amd.framework.driver import SchedulerDriver
 from dcos_commons_amd.mesos import protos as P
@@ -115,6 +115,7 @@ class V1HttpSchedulerDriver(SchedulerDriver):
         self._outbox_cond = threading.Condition()
         self._in_flight = 0
         self._sender: Optional[threading.Thread] = None
+        self._status_gate: Optional[Callable[[], None]] = None
 
     # -- lifecycle ---------------------------------------------------------------------
     @property
@@ -197,13 +198,9 @@ class V1HttpSchedulerDriver(SchedulerDriver):
         self._send(P.Call(type=P.Call.SUPPRESS))
 
     def acknowledge_status_update(self, status: P.TaskStatus) -> None:
-        if not status.uuid or not status.HasField("agent_id"):
-            return
-        call = P.Call(type=P.Call.ACKNOWLEDGE)
-        call.acknowledge.agent_id.CopyFrom(status.agent_id)
-        call.acknowledge.task_id.CopyFrom(status.task_id)
-        call.acknowledge.uuid = status.uuid
-        self._send(call)
+        call = self._ack_call(status)
+        if call is not None:
+            self._send(call)
 
     def send_framework_message(self, executor_id: P.ExecutorID, agent_id: P.AgentID, data: bytes) -> None:
         call = P.Call(type=P.Call.MESSAGE)
@@ -436,15 +433,22 @@ class V1HttpSchedulerDriver(SchedulerDriver):
             if chunks is not None and chunks.done:
                 return
 
+    def set_status_gate(self, gate: Optional[Callable[[], None]]) -> None:
+        """``gate()`` runs on the event thread before each status callback and may block it (the
+        framework's offer-cycle gate); the thread holds no lock of the scheduler's there."""
+        self._status_gate = gate
+
     def _on_updates(self, statuses: List[P.TaskStatus]) -> None:
+        gate = self._status_gate
+        if gate is not None:
+            gate()
         if len(statuses) == 1 or getattr(self.scheduler, "status_updates", None) is None:
             for status in statuses:
                 self._on_update(status)
             return
         self._call_scheduler("status_updates", statuses)
         if self.implicit_acknowledgements:
-            for status in statuses:
-                self._acknowledge(status)
+            self._acknowledge_all(statuses)
 
     def _on_update(self, status: P.TaskStatus) -> None:
         self._call_scheduler("status_update", status)
@@ -456,6 +460,21 @@ class V1HttpSchedulerDriver(SchedulerDriver):
             self.acknowledge_status_update(status)
         except MesosCallError as e:
             LOGGER.warning("ACKNOWLEDGE of %s failed: %s", status.task_id.value, e)
+
+    def _acknowledge_all(self, statuses: List[P.TaskStatus]) -> None:
+        """The ACKNOWLEDGEs of a batch of updates (one call each over HTTP)."""
+        for status in statuses:
+            self._acknowledge(status)
+
+    @staticmethod
+    def _ack_call(status: P.TaskStatus) -> Optional[P.Call]:
+        if not status.uuid or not status.HasField("agent_id"):
+            return None
+        call = P.Call(type=P.Call.ACKNOWLEDGE)
+        call.acknowledge.agent_id.CopyFrom(status.agent_id)
+        call.acknowledge.task_id.CopyFrom(status.task_id)
+        call.acknowledge.uuid = status.uuid
+        return call
 
     def _call_scheduler(self, name: str, *args) -> None:
         fn = getattr(self.scheduler, name, None)
@@ -487,7 +506,7 @@ class V1HttpSchedulerDriver(SchedulerDriver):
         elif t == P.Event.RESCIND:
             self._call_scheduler("offer_rescinded", ev.rescind.offer_id)
         elif t == P.Event.UPDATE:
-            self._on_update(ev.update.status)
+            self._on_updates([ev.update.status])
         elif t == P.Event.MESSAGE:
             m = ev.message
             self._call_scheduler("framework_message", m.executor_id, m.agent_id, m.data)

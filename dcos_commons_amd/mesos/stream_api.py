@@ -285,6 +285,12 @@ class StreamMaster:
 
 
 # -- scheduler side ------------------------------------------------------------------------
+def _with_fid(call: P.Call, fid: Optional[str]) -> P.Call:
+    if fid:
+        call.framework_id.value = fid
+    return call
+
+
 class StreamSchedulerDriver(V1HttpSchedulerDriver):
     """``SchedulerDriver`` over the framed stream: the callbacks, acknowledgements and update
     batching of ``V1HttpSchedulerDriver``, its HTTP transport replaced by one socket. A call is
@@ -362,6 +368,32 @@ class StreamSchedulerDriver(V1HttpSchedulerDriver):
                 sock.sendall(data)
             except OSError as e:
                 raise MesosCallError(0, str(e)) from e
+
+    def _acknowledge_all(self, statuses: List[P.TaskStatus]) -> None:
+        """A batch's ACKNOWLEDGEs leave in one write: one frame per call, so the master reads
+        them as one batch (its reader hands every frame of a read over together)."""
+        calls = [c for c in map(self._ack_call, statuses) if c is not None]
+        if len(calls) < 2:
+            for c in calls:
+                self._send_quiet(c)
+            return
+        fid = self._framework_id
+        data = b"".join(frame(_with_fid(c, fid).SerializeToString()) for c in calls)
+        with self._wlock:
+            sock = self._sock
+            if sock is None or self.stream_id is None:
+                LOGGER.warning("ACKNOWLEDGE of %d update(s) dropped: not subscribed", len(calls))
+                return
+            try:
+                sock.sendall(data)
+            except OSError as e:
+                LOGGER.warning("ACKNOWLEDGE of %d update(s) failed: %s", len(calls), e)
+
+    def _send_quiet(self, call: P.Call) -> None:
+        try:
+            self._send_now(call)
+        except MesosCallError as e:
+            LOGGER.warning("ACKNOWLEDGE of %s failed: %s", call.acknowledge.task_id.value, e)
 
     def flush(self, timeout_s: float = 10.0) -> bool:
         return True

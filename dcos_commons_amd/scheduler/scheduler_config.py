@@ -297,6 +297,12 @@ class SchedulerConfig:
         """Wake the offer loop on every status update (reference: poll only)."""
         return self.env.get_optional_boolean("SDK_EVENT_DRIVEN", True)
 
+    def status_cycle_wait_s(self) -> float:
+        """How long a status update read from a network driver waits for a running offer cycle
+        to finish before it is handled (``SDK_STATUS_CYCLE_WAIT_MS``; 0 = handle it at once, as the
+        reference's driver callbacks do). See ``OfferProcessor.wait_cycle_idle``."""
+        return self.env.get_optional_double("SDK_STATUS_CYCLE_WAIT_MS", 100.0) / 1000.0
+
     def offer_hold_s(self) -> float:
         """Hold unused offers this long while WORKING instead of declining them for 1 h
         (0 = reference behaviour: long decline + rate-limited revive)."""

@@ -30,6 +30,7 @@ REFERENCE_SEMANTICS: Dict[str, str] = {
     "SDK_STREAM_LAUNCHES": "false",
     "SDK_REVIVE_ONLY_UNMATCHED": "false",
     "SDK_GC_GEN0_THRESHOLD": "0",
+    "SDK_STATUS_CYCLE_WAIT_MS": "0",
 }
 
 PROFILES: Dict[str, Dict[str, str]] = {"mi355x": {}, "reference": REFERENCE_SEMANTICS}
