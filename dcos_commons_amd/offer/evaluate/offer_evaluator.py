@@ -123,18 +123,29 @@ class OfferEvaluator:
         environment, checks, labels and container info, and the executor. Building it renders the
         pod's whole task environment (a reference hdfs or cassandra task carries hundreds of
         variables), so it is built once per (pod instance, target config, requirement env, goal
-        overrides) and every evaluation -- each offer cycle, each offer -- works on a copy."""
+        overrides) and every evaluation -- each offer cycle, each offer -- works on a copy. The
+        first instance's template is also kept per pod type: the other instances are moved from it
+        (``PodInfoBuilder.for_instance``), so an N-pod parallel deploy renders the tasks once."""
         pi = requirement.pod_instance
-        key = (pi.pod.type, pi.index, str(target_config), tuple(sorted(requirement.environment.items())),
-               tuple(sorted((k, str(v)) for k, v in override_map.items())), fid_proto.value)
+        shared = (pi.pod.type, str(target_config), tuple(sorted(requirement.environment.items())),
+                  tuple(sorted((k, str(v)) for k, v in override_map.items())), fid_proto.value)
+        key = (pi.index,) + shared
         hit = self._templates.get(key)
         if hit is not None and hit[0] is pi.pod:
             self._templates.move_to_end(key)
             return hit[1]
-        tpl = PodInfoBuilder(requirement, self.service_name, target_config, self.template_url_factory,
-                             self.scheduler_config, (), fid_proto, override_map)
+        tpl = None
+        # another instance of the pod with the same inputs: move its template to this index
+        # (PodInfoBuilder.for_instance) instead of rendering every task again
+        sibling = self._templates.get(shared)
+        if sibling is not None and sibling[0] is pi.pod:
+            tpl = sibling[1].for_instance(pi)
+        if tpl is None:
+            tpl = PodInfoBuilder(requirement, self.service_name, target_config, self.template_url_factory,
+                                 self.scheduler_config, (), fid_proto, override_map)
+            self._templates[shared] = (pi.pod, tpl)
         self._templates[key] = (pi.pod, tpl)
-        if len(self._templates) > self._TEMPLATE_CACHE_SIZE:
+        while len(self._templates) > self._TEMPLATE_CACHE_SIZE:
             self._templates.popitem(last=False)
         return tpl
 

@@ -71,6 +71,42 @@ def _environment_bytes(service_name: str, pod_instance: PodInstance, task_spec: 
     return L.env_template(static).encode(extra)
 
 
+def _move_environment(env: P.Environment, old_name: str, new_name: str, index: str, tail: int = 0) -> bool:
+    """Rewrites the per-instance variables of a task environment in place (see
+    ``PodInfoBuilder.for_instance``); False when the result would not be what a fresh build
+    gives."""
+    vs = env.variables
+    slot = -1
+    fixed = 0
+    for i, v in enumerate(vs):
+        name = v.name
+        if name == old_name:
+            if slot >= 0:
+                return False
+            slot = i
+        elif name == new_name:
+            return False
+        elif name == L.POD_INSTANCE_INDEX_TASKENV:
+            v.value = index
+            fixed += 1
+        elif name == L.TASK_NAME_TASKENV:
+            v.value = new_name
+            fixed += 1
+    if slot < 0 or fixed != 2:
+        return False
+    # the task-name variable keeps its slot only if the new name sorts there too, among the
+    # name-sorted variables (the last ``tail`` ones were appended after them)
+    end = len(vs) - tail
+    if slot >= end:
+        return False
+    if slot > 0 and not vs[slot - 1].name < new_name:
+        return False
+    if slot + 1 < end and not new_name < vs[slot + 1].name:
+        return False
+    vs[slot].name = new_name
+    return True
+
+
 def config_template_download_path(config: ConfigFileSpec) -> str:
     return CONFIG_TEMPLATE_DOWNLOAD_PATH + config.name
 
@@ -86,6 +122,9 @@ class PodInfoBuilder:
                  current_pod_tasks, framework_id: P.FrameworkID, override_map: Dict[str, GoalStateOverride]):
         pi: PodInstance = requirement.pod_instance
         self.pod_instance = pi
+        # variables appended after a command environment's name-sorted part: the requirement's
+        # environment, then the pod's environment secrets (for_instance)
+        self._env_tail = len(requirement.environment) + sum(1 for x in pi.pod.secrets if x.env_key is not None)
         self.assigned_overlay_ports: Set[int] = set()
         self.task_builders: Dict[str, P.TaskInfo] = {}
         for ts in pi.pod.tasks:
@@ -120,6 +159,7 @@ class PodInfoBuilder:
         Call it on a builder no stage has touched."""
         c = PodInfoBuilder.__new__(PodInfoBuilder)
         c.pod_instance = self.pod_instance
+        c._env_tail = self._env_tail
         c.assigned_overlay_ports = set(self.assigned_overlay_ports)
         c.task_builders = {}
         for name, tb in self.task_builders.items():
@@ -129,6 +169,52 @@ class PodInfoBuilder:
         c.executor_builder = P.ExecutorInfo()
         c.executor_builder.CopyFrom(self.executor_builder)
         c.ports_by_task = self.ports_by_task  # read-only after construction
+        return c
+
+    def for_instance(self, pi: PodInstance) -> Optional["PodInfoBuilder"]:
+        """This untouched template moved to another instance of the same pod (same requirement
+        environment, target config and goal overrides), or None where that cannot be done exactly.
+
+        A fresh builder for instance ``pi`` differs from this one's copy only in what the pod
+        index reaches: each task's name, its ``index`` label, its discovery name, and in the task
+        environments (command, health check, readiness check) the ``POD_INSTANCE_INDEX`` and
+        ``TASK_NAME`` values and the variable named after the task. That variable sits in the
+        name-sorted part of the environment; when the new name does not sort into the old slot,
+        or a name is ambiguous, the caller builds from scratch. A parallel deploy of N instances
+        builds the pod's task templates once instead of N times."""
+        old = self.pod_instance
+        if pi.pod is not old.pod:
+            return None
+        c = self.clone()
+        c.pod_instance = pi
+        index = str(pi.index)
+        for ts in pi.pod.tasks:
+            t = c.task_builders.get(ts.name)
+            if t is None:
+                return None
+            old_name, new_name = f"{old.name}-{ts.name}", f"{pi.name}-{ts.name}"
+            if t.name != old_name:
+                return None
+            t.name = new_name
+            found = 0
+            for label in t.labels.labels:
+                if label.key == L.TASK_INDEX_LABEL:
+                    label.value = index
+                    found += 1
+            if found != 1:
+                return None
+            if ts.discovery is not None and ts.discovery.prefix:
+                t.discovery.name = f"{ts.discovery.prefix}-{pi.index}"
+            envs = []
+            if t.HasField("command"):
+                envs.append((t.command.environment, self._env_tail))
+            if t.HasField("health_check"):
+                envs.append((t.health_check.command.environment, 0))
+            if t.HasField("check"):
+                envs.append((t.check.command.command.environment, 0))
+            for env, tail in envs:
+                if not _move_environment(env, old_name, new_name, index, tail):
+                    return None
         return c
 
     # -- accessors ---------------------------------------------------------------------

@@ -578,6 +578,12 @@ def test_in_place_relaunch_skips_offers_without_its_reservations():
     assert ops(again) == [L, None] and again[0].offer.id.value == "full"
 
 
+def _instance_templates(evaluator):
+    """The evaluator's per-instance templates (its cache also keeps one per pod type, keyed
+    without the index, to move to other instances)."""
+    return {k: v for k, v in evaluator._templates.items() if isinstance(k[0], int)}
+
+
 def test_pod_templates_are_reused_across_evaluations_without_leaking_offer_state():
     """The evaluator keeps one untouched PodInfoBuilder template per (pod instance, target config,
     requirement env, goal overrides) and each evaluation works on a copy: task IDs, agent IDs,
@@ -586,10 +592,11 @@ def test_pod_templates_are_reused_across_evaluations_without_leaking_offer_state
     o1 = complete_offer(scalar("cpus", 1.0), ranges("ports", (5000, 5000)), agent="a1", oid="o1")
     o2 = complete_offer(scalar("cpus", 1.0), ranges("ports", (6000, 6000)), agent="a2", oid="o2")
     first = of(f.evaluate([o1]), LaunchOfferRecommendation)[0].task_info
-    assert len(f.evaluator._templates) == 1
-    tpl = next(iter(f.evaluator._templates.values()))[1]
+    assert len(_instance_templates(f.evaluator)) == 1
+    tpl = next(iter(_instance_templates(f.evaluator).values()))[1]
     second = of(f.evaluate([o2]), LaunchOfferRecommendation)[0].task_info
-    assert len(f.evaluator._templates) == 1 and next(iter(f.evaluator._templates.values()))[1] is tpl
+    assert len(_instance_templates(f.evaluator)) == 1
+    assert next(iter(_instance_templates(f.evaluator).values()))[1] is tpl
     assert first.task_id.value != second.task_id.value
     assert (first.agent_id.value, second.agent_id.value) == ("a1", "a2")
     assert env_to_map(first.command.environment)["PORT_HTTP"] == "5000"
@@ -600,4 +607,28 @@ def test_pod_templates_are_reused_across_evaluations_without_leaking_offer_state
     # another pod index, requirement environment or target config is another template
     f.evaluator.evaluate(PodInstanceRequirement(PodInstance(f.spec.pods[0], 0), ["server"],
                                                 environment={"EXTRA": "1"}), [o1])
-    assert len(f.evaluator._templates) == 2
+    assert len(_instance_templates(f.evaluator)) == 2
+
+
+def test_other_instances_of_a_pod_are_moved_from_its_first_template(monkeypatch):
+    """Index 1 of a pod whose index 0 was evaluated with the same inputs gets index 0's template
+    moved to it (PodInfoBuilder.for_instance) instead of a fresh build; what it launches is what
+    a fresh build launches (tests/test_template_instances.py checks the templates byte for byte)."""
+    from dcos_commons_amd.offer.evaluate import pod_info_builder as PIB
+
+    f = Fixture(server())
+    o1 = complete_offer(scalar("cpus", 1.0), agent="a1", oid="o1")
+    f.evaluate([o1])
+    builds = []
+    orig = PIB.PodInfoBuilder.__init__
+
+    def counting(self, *a, **k):
+        builds.append(1)
+        orig(self, *a, **k)
+    monkeypatch.setattr(PIB.PodInfoBuilder, "__init__", counting)
+    rec = of(f.evaluator.evaluate(PodInstanceRequirement(PodInstance(f.spec.pods[0], 1), ["server"]), [o1]),
+             LaunchOfferRecommendation)[0].task_info
+    assert not builds
+    assert rec.name == f"{f.spec.pods[0].type}-1-server"
+    env = env_to_map(rec.command.environment)
+    assert env["POD_INSTANCE_INDEX"] == "1" and env["TASK_NAME"] == rec.name and env[rec.name] == "true"
