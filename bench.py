@@ -50,8 +50,8 @@ def parse_args(argv=None):
                          "master process; each rank, or a helper process per agent, runs its tasks), the "
                          "scheduler here over the framed v1 stream; inprocess: one interpreter holds all of it")
     ap.add_argument("--agent0", default="thread", choices=["thread", "process"],
-                    help="split topology without torchrun: agent 0 runs on a thread of this process (thread) or in "
-                         "a helper process like the others (process)")
+                    help="split topology: agent 0 (rank 0's agent under torchrun) runs on a thread of this "
+                         "process (thread) or in a process of its own like the others (process)")
     ap.add_argument("--cluster-switch-interval-ms", type=float, default=0.0,
                     help="split topology: interpreter switch interval of the master and agent processes "
                          "(0: Python's 5 ms)")

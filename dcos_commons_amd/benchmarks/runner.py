@@ -380,7 +380,10 @@ def _run_distributed_split(args, rank, world, local_rank, use_gpu, dist, cluster
     record = os.environ.get("SDK_BENCH_RECORD")
     checks: list = []
     info = _local_agent_info(rank, local_rank, device)
-    agent = _start_agent_thread(host, ports["agents"], info, _agent_check(device, use_gpu, checks))
+    agent = None
+    if rank != 0 or getattr(args, "agent0", "thread") != "process":
+        agent = _start_agent_thread(host, ports["agents"], info, _agent_check(device, use_gpu, checks))
+    # else: rank 0's agent is the process SplitCluster started for it (--agent0 process)
 
     def barrier():
         _sync()
@@ -419,7 +422,8 @@ def _run_distributed_split(args, rank, world, local_rank, use_gpu, dist, cluster
     t = torch.tensor([elapsed], dtype=torch.float64, device=coll_dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     client.call("shutdown")
-    agent.join(30)
+    if agent is not None:
+        agent.join(30)
     specs = [agent_spec_from_registration(x, i) for i, x in enumerate(infos)]
     _record(record, {"rank": 0, "device": device, "registered": info, "checks": checks, "placement": placement,
                      "agents": [_spec_view(s) for s in specs], "elapsed_local_s": elapsed,

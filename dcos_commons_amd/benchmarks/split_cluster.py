@@ -5,6 +5,8 @@
 * without ``torchrun`` and with ``--gpus N > 1`` it also starts N-1 agent processes
   (``parallel.agent_process``), so that, as under ``torchrun`` where every rank is one, every agent
   is a process of its own that runs its tasks' lifecycle and readiness checks;
+* with ``--agent0 process`` agent 0 is a process too (rank 0's agent under ``torchrun``), instead
+  of a thread in the scheduler's interpreter;
 * the scheduler stays in the bench process and subscribes over ``mesos.stream_api``.
 
 A process that has initialised a GPU must not start programs (the box forbids the exec), which is
@@ -35,8 +37,16 @@ class SplitCluster:
         si = getattr(args, "cluster_switch_interval_ms", 0.0) or 0.0
         master, ports = master_process.spawn(args.allocation_interval, host=host, switch_interval_ms=si)
         procs = [master]
-        first = 0 if getattr(args, "agent0", "thread") == "process" else 1
-        if world == 1 and args.gpus > first:
+        agent0_process = getattr(args, "agent0", "thread") == "process"
+        first = 0 if agent0_process else 1
+        # agent processes: without torchrun, agents first..N-1 (agent 0 is this process's thread
+        # unless --agent0 process); under torchrun every other rank is an agent, and --agent0
+        # process moves rank 0's own agent out of the scheduler's interpreter
+        if world == 1:
+            ranks = list(range(first, args.gpus))
+        else:
+            ranks = [0] if agent0_process else []
+        if ranks:
             probe = "off"
             if not args.no_gpu_probe:
                 import torch
@@ -48,8 +58,10 @@ class SplitCluster:
             root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
             env = dict(os.environ)
             env["PYTHONPATH"] = root + (os.pathsep + env["PYTHONPATH"] if env.get("PYTHONPATH") else "")
-            for i in range(first, args.gpus):
-                dev = i % ndev if ndev else i
+            local = int(os.environ.get("LOCAL_RANK", "0")) if world > 1 else None
+            for i in ranks:
+                dev = (local if local is not None else i)
+                dev = dev % ndev if ndev else dev
                 procs.append(subprocess.Popen(
                     [sys.executable, "-m", "dcos_commons_amd.parallel.agent_process", "--host", host,
                      "--port", str(ports["agents"]), "--rank", str(i), "--device", str(dev), "--probe", probe,

@@ -23,14 +23,23 @@ ap = argparse.ArgumentParser()
 ap.add_argument("n", type=int)
 ap.add_argument("--probe", action="store_true")
 ap.add_argument("--cycles", type=int, default=5)
+ap.add_argument("--agent0", choices=["process", "thread"], default="process",
+                help="agent 0 in a process of its own, or on a thread of the scheduler's process (as bench.py's "
+                     "default)")
 args = ap.parse_args()
 
 proc, ports = MP.spawn()
 client = MP.MasterClient("127.0.0.1", ports["control"])
 root = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+first = 1 if args.agent0 == "thread" else 0
 kids = [subprocess.Popen([sys.executable, "-m", "dcos_commons_amd.parallel.agent_process", "--port",
                           str(ports["agents"]), "--rank", str(i), "--device", "0", "--probe",
-                          "on" if args.probe else "off"], cwd=root) for i in range(args.n)]
+                          "on" if args.probe else "off"], cwd=root) for i in range(first, args.n)]
+if first:
+    from dcos_commons_amd.benchmarks.runner import _local_agent_info, _start_agent_thread  # noqa: E402
+    from dcos_commons_amd.parallel.agent_process import check_for  # noqa: E402
+
+    _start_agent_thread("127.0.0.1", ports["agents"], _local_agent_info(0, 0, 0), check_for(0, args.probe))
 client.call("agents", n=args.n)
 
 cpu = collections.defaultdict(float)

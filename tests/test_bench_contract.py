@@ -104,13 +104,15 @@ def test_bench_four_ranks_build_agents_from_what_each_rank_registers(tmp_path):
 
 
 @pytest.mark.timeout(300)
-def test_bench_two_ranks_over_gloo():
+@pytest.mark.parametrize("agent0", ["thread", "process"])
+def test_bench_two_ranks_over_gloo(agent0):
+    """Two ranks; rank 0's agent on a thread of the scheduler's process or in a process of its own."""
     env = dict(os.environ, PYTHONPATH=ROOT, MASTER_ADDR="127.0.0.1", OMP_NUM_THREADS="1")
     env.pop("CUDA_VISIBLE_DEVICES", None)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
            os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "1", "--warmup", "1", "--no-gpu-probe",
-           "--allocation-interval", "0.05"]
+           "--allocation-interval", "0.05", "--agent0", agent0]
     p = subprocess.run(cmd, capture_output=True, text=True, timeout=280, env=env, cwd=ROOT)
     assert p.returncode == 0, p.stderr[-3000:]
     recs = _json_lines(p.stdout)
