@@ -298,3 +298,41 @@ def test_agent_runtime_gates_readiness_on_the_hip_probe():
     finally:
         stream.stop()
         master.shutdown()
+
+
+def test_runtime_reports_running_before_a_check_unless_checks_are_fast(monkeypatch):
+    """STARTING / RUNNING leave before the first check; once this agent's checks finish within
+    the report window they leave together with the check's result; after a slow check they go
+    first again."""
+    monkeypatch.setenv("SDK_AGENT_REPORT_WINDOW_MS", "50")
+    reports = []
+    delay = {"s": 0.0}
+
+    def check(devices):
+        time.sleep(delay["s"])
+        return True
+    rt = AgentRuntime(lambda reps: reports.append([r["event"] for r in reps]), check)
+    try:
+        def launch(tid):
+            reports.clear()
+            rt.handle({"op": "launch", "task": tid, "name": tid, "devices": [0], "check": {"delay": 0, "interval": 1},
+                       "timing": {}})
+            return list(reports)
+        assert launch("t1") == [["starting", "running"], ["ready"]]          # nothing known yet: RUNNING first
+        assert launch("t2") == [["starting", "running", "ready"]]            # fast checks: one report
+        delay["s"] = 0.08
+        assert launch("t3") == [["starting", "running", "ready"]]            # looked fast; this one was slow
+        delay["s"] = 0.0
+        assert launch("t4") == [["starting", "running"], ["ready"]]          # after a slow check: RUNNING first
+    finally:
+        rt.shutdown()
+    monkeypatch.setenv("SDK_AGENT_REPORT_WINDOW_MS", "0")
+    rt = AgentRuntime(lambda reps: reports.append([r["event"] for r in reps]), lambda d: True)
+    try:
+        for tid in ("a", "b"):
+            reports.clear()
+            rt.handle({"op": "launch", "task": tid, "name": tid, "devices": [0], "check": {"delay": 0, "interval": 1},
+                       "timing": {}})
+            assert reports == [["starting", "running"], ["ready"]]           # window 0: always RUNNING first
+    finally:
+        rt.shutdown()
