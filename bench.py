@@ -49,7 +49,7 @@ def parse_args(argv=None):
                     help="split: the master and every agent's task lifecycle run in processes of their own (a "
                          "master process; each rank, or a helper process per agent, runs its tasks), the "
                          "scheduler here over the framed v1 stream; inprocess: one interpreter holds all of it")
-    ap.add_argument("--agent0", default="thread", choices=["thread", "process"],
+    ap.add_argument("--agent0", default="process", choices=["thread", "process"],
                     help="split topology: agent 0 (rank 0's agent under torchrun) runs on a thread of this "
                          "process (thread) or in a process of its own like the others (process)")
     ap.add_argument("--cluster-switch-interval-ms", type=float, default=0.0,

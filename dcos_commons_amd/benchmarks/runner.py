@@ -318,6 +318,7 @@ def _split_summary(args, n, cycles, elapsed, use_gpu, parallelism, infos):
     out = _summary(args, n, cycles, elapsed, use_gpu, parallelism)
     out["config"]["topology"] = ("split: master process; each agent (rank or helper process) runs its tasks' "
                                  "lifecycle and readiness checks; scheduler over the framed v1 stream")
+    out["config"]["agent0"] = getattr(args, "agent0", "process")
     out["config"]["agent_attributes"] = agent_spec_from_registration(infos[0], 0).attributes
     return out
 
@@ -331,7 +332,7 @@ def _run_single_split(args, n, use_gpu, cluster):
     checks: list = []
     info = _local_agent_info(0, 0, 0)
     agent = None
-    if getattr(args, "agent0", "thread") == "thread":
+    if getattr(args, "agent0", "process") == "thread":
         agent = _start_agent_thread(cluster.host, cluster.ports["agents"], info, _agent_check(0, use_gpu, checks))
     client = MasterClient(cluster.host, cluster.ports["control"])
     infos = client.call("agents", n=n)
@@ -381,7 +382,7 @@ def _run_distributed_split(args, rank, world, local_rank, use_gpu, dist, cluster
     checks: list = []
     info = _local_agent_info(rank, local_rank, device)
     agent = None
-    if rank != 0 or getattr(args, "agent0", "thread") != "process":
+    if rank != 0 or getattr(args, "agent0", "process") != "process":
         agent = _start_agent_thread(host, ports["agents"], info, _agent_check(device, use_gpu, checks))
     # else: rank 0's agent is the process SplitCluster started for it (--agent0 process)
 

@@ -2,11 +2,12 @@
 
 * rank 0 (or the only process) starts the master process (``mesos.master_process``): offers,
   reservations, ACCEPTs and status forwarding, as a Mesos master;
-* without ``torchrun`` and with ``--gpus N > 1`` it also starts N-1 agent processes
-  (``parallel.agent_process``), so that, as under ``torchrun`` where every rank is one, every agent
-  is a process of its own that runs its tasks' lifecycle and readiness checks;
-* with ``--agent0 process`` agent 0 is a process too (rank 0's agent under ``torchrun``), instead
-  of a thread in the scheduler's interpreter;
+* it starts the agent processes (``parallel.agent_process``) that are not ranks: without
+  ``torchrun``, all N agents; under ``torchrun``, rank 0's own agent (the other ranks are agents
+  themselves). So every agent is a process of its own that runs its tasks' lifecycle and readiness
+  checks, and the scheduler's interpreter runs only the scheduler, as on a cluster. ``--agent0
+  thread`` keeps agent 0 on a thread of the bench process instead (same-box A/B: 1 pod 2.04 ->
+  1.90 ms, 8 pods 5.81 -> 5.57 ms with the process, ``profiles/agent0_ab_r06_box.txt``);
 * the scheduler stays in the bench process and subscribes over ``mesos.stream_api``.
 
 A process that has initialised a GPU must not start programs (the box forbids the exec), which is
@@ -37,7 +38,7 @@ class SplitCluster:
         si = getattr(args, "cluster_switch_interval_ms", 0.0) or 0.0
         master, ports = master_process.spawn(args.allocation_interval, host=host, switch_interval_ms=si)
         procs = [master]
-        agent0_process = getattr(args, "agent0", "thread") == "process"
+        agent0_process = getattr(args, "agent0", "process") == "process"
         first = 0 if agent0_process else 1
         # agent processes: without torchrun, agents first..N-1 (agent 0 is this process's thread
         # unless --agent0 process); under torchrun every other rank is an agent, and --agent0

@@ -661,8 +661,8 @@ class OfferProcessor:
                 for o in new_offers:
                     self._in_progress.discard(o.id.value)
 
-    def wait_cycle_idle(self, timeout_s: float) -> None:
-        """Blocks while an offer cycle is evaluating, for at most ``timeout_s``.
+    def wait_cycle_idle(self, timeout_s: float) -> bool:
+        """Blocks while an offer cycle is evaluating, for at most ``timeout_s``; True if it waited.
 
         The scheduler's threads share one interpreter lock. A status batch handled while a cycle
         runs takes that lock whenever the cycle releases it (every ACCEPT written to the master
@@ -672,8 +672,10 @@ class OfferProcessor:
         a cycle waits for a status, so the statuses that queue up meanwhile are handled in one
         batch when it ends, and the last pod's launch leaves that much earlier."""
         with self._cycle_cv:
-            if self._cycle_active:
-                self._cycle_cv.wait_for(lambda: not self._cycle_active, timeout_s)
+            if not self._cycle_active:
+                return False
+            self._cycle_cv.wait_for(lambda: not self._cycle_active, timeout_s)
+            return True
 
     def _reoffer_revive(self) -> bool:
         self.revive_manager.request_revive(bypass_spacing=True)

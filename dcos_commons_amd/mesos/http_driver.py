@@ -115,7 +115,7 @@ class V1HttpSchedulerDriver(SchedulerDriver):
         self._outbox_cond = threading.Condition()
         self._in_flight = 0
         self._sender: Optional[threading.Thread] = None
-        self._status_gate: Optional[Callable[[], None]] = None
+        self._status_gate: Optional[Callable[[], bool]] = None
 
     # -- lifecycle ---------------------------------------------------------------------
     @property
@@ -433,9 +433,10 @@ class V1HttpSchedulerDriver(SchedulerDriver):
             if chunks is not None and chunks.done:
                 return
 
-    def set_status_gate(self, gate: Optional[Callable[[], None]]) -> None:
+    def set_status_gate(self, gate: Optional[Callable[[], bool]]) -> None:
         """``gate()`` runs on the event thread before each status callback and may block it (the
-        framework's offer-cycle gate); the thread holds no lock of the scheduler's there."""
+        framework's offer-cycle gate; True when it did); the thread holds no lock of the
+        scheduler's there."""
         self._status_gate = gate
 
     def _on_updates(self, statuses: List[P.TaskStatus]) -> None:

@@ -51,26 +51,46 @@ class FrameReader:
         self._buf = bytearray()
 
     def batches(self) -> Iterator[List[bytes]]:
-        buf = self._buf
         while True:
             data = self.sock.recv(self.bufsize)
             if not data:
                 return
-            buf += data
-            out = []
-            pos = 0
-            while len(buf) - pos >= 4:
-                (n,) = _LEN.unpack_from(buf, pos)
-                if n > MAX_FRAME:
-                    raise OSError(f"frame of {n} bytes exceeds the {MAX_FRAME}-byte limit")
-                if len(buf) - pos - 4 < n:
-                    break
-                out.append(bytes(buf[pos + 4:pos + 4 + n]))
-                pos += 4 + n
-            if pos:
-                del buf[:pos]
+            self._buf += data
+            out = self._complete()
             if out:
                 yield out
+
+    def ready(self) -> List[bytes]:
+        """The complete frames that have arrived by now, without blocking (a reader that waited
+        before handling its batch picks up what queued up meanwhile). An end of stream seen here
+        is seen again by the next blocking read."""
+        while True:
+            try:
+                data = self.sock.recv(self.bufsize, socket.MSG_DONTWAIT)
+            except (BlockingIOError, InterruptedError):
+                break
+            if not data:
+                break
+            self._buf += data
+            if len(data) < self.bufsize:
+                break
+        return self._complete()
+
+    def _complete(self) -> List[bytes]:
+        buf = self._buf
+        out = []
+        pos = 0
+        while len(buf) - pos >= 4:
+            (n,) = _LEN.unpack_from(buf, pos)
+            if n > MAX_FRAME:
+                raise OSError(f"frame of {n} bytes exceeds the {MAX_FRAME}-byte limit")
+            if len(buf) - pos - 4 < n:
+                break
+            out.append(bytes(buf[pos + 4:pos + 4 + n]))
+            pos += 4 + n
+        if pos:
+            del buf[:pos]
+        return out
 
 
 def _nodelay(sock: socket.socket) -> None:
@@ -321,12 +341,19 @@ class StreamSchedulerDriver(V1HttpSchedulerDriver):
                     sock.sendall(frame(self._subscribe_call().SerializeToString()))
                 self.stream_id = "stream"
                 backoff = self.backoff_s
-                for batch in FrameReader(sock).batches():
+                reader = FrameReader(sock)
+                for batch in reader.batches():
                     if self._stopped.is_set():
                         break
+                    events = [P.Event.FromString(data) for data in batch]
+                    gate = self._status_gate
+                    if gate is not None and any(ev.type == P.Event.UPDATE for ev in events):
+                        # a status waits for a running offer cycle (FrameworkScheduler's gate);
+                        # what arrived meanwhile joins this batch, so it is handled in one go
+                        if gate():
+                            events.extend(P.Event.FromString(data) for data in reader.ready())
                     updates: List[P.TaskStatus] = []
-                    for data in batch:
-                        ev = P.Event.FromString(data)
+                    for ev in events:
                         if ev.type == P.Event.UPDATE:
                             updates.append(ev.update.status)
                             continue

@@ -10,13 +10,17 @@ process itself is agent 0), so every agent is a separate process, as on a cluste
 from __future__ import annotations
 
 import argparse
+import json
 import logging
+import os
 import sys
+from typing import Optional
 
 
-def check_for(device: int, probe: bool):
+def check_for(device: int, probe: bool, checks: Optional[list] = None):
     """``check(msg) -> (ok, detail)`` for the agent link: the fused HIP readiness probe on
-    ``device`` (``probe``; a missing extension then fails loudly), else a synthetic pass."""
+    ``device`` (``probe``; a missing extension then fails loudly), else a synthetic pass. Each
+    check is appended to ``checks`` as (assigned devices, device, ok)."""
     runner = None
     if probe:
         from dcos_commons_amd.benchmarks.runner import gpu_check_runner
@@ -26,10 +30,13 @@ def check_for(device: int, probe: bool):
     def check(msg):
         assigned = list(msg.get("devices") or [device])
         if assigned != [device]:
+            if checks is not None:
+                checks.append((assigned, device, False))
             return False, f"check for devices {assigned} sent to the agent of device {device}"
-        if runner is None:
-            return True, f"synthetic on device {device}"
-        return bool(runner(None, [device])), f"probe on device {device}"
+        ok = True if runner is None else bool(runner(None, [device]))
+        if checks is not None:
+            checks.append((assigned, device, ok))
+        return ok, f"{'probe' if runner is not None else 'synthetic'} on device {device}"
     check.probing = runner is not None
     return check
 
@@ -52,7 +59,14 @@ def main(argv=None) -> int:
     from dcos_commons_amd.parallel import agent_link
 
     info = _local_agent_info(args.rank, args.rank, args.device)
-    agent_link.run_agent(args.host, args.port, info, check_for(args.device, args.probe == "on"))
+    checks: list = []
+    agent_link.run_agent(args.host, args.port, info, check_for(args.device, args.probe == "on", checks))
+    record = os.environ.get("SDK_BENCH_RECORD")
+    if record:
+        # the bench's per-rank records (runner._record) get this agent's checks next to them
+        os.makedirs(record, exist_ok=True)
+        with open(os.path.join(record, f"agent{args.rank}.json"), "w") as f:
+            json.dump({"rank": args.rank, "device": args.device, "registered": info, "checks": checks}, f)
     return 0
 
 

@@ -84,8 +84,10 @@ def test_bench_four_ranks_build_agents_from_what_each_rank_registers(tmp_path):
     for r, data in ranks.items():
         assert data["device"] == r and data["registered"]["devices"] == [r]
         assert data["registered"]["attributes"]["xgmi_hive"] == hive[r]
-        # every check this rank served was for its own device, and ran there
-        assert data["checks"] and all(a == [r] and d == r and ok for a, d, ok in data["checks"])
+        # every check this rank served was for its own device, and ran there (rank 0's agent is a
+        # process of its own by default: its checks are in its own record)
+        checks = data["checks"] or json.load(open(record / f"agent{r}.json"))["checks"]
+        assert checks and all(tuple(a) == (r,) and d == r and ok for a, d, ok in checks)
     # the agents rank 0 offered are exactly what the ranks registered
     agents = {a["hostname"]: a for a in ranks[0]["agents"]}
     for r, data in ranks.items():
@@ -148,12 +150,13 @@ def test_deploy_bench_waits_on_status_events():
 
 @pytest.mark.timeout(300)
 def test_bench_single_process_with_agent_processes(tmp_path):
-    """``--gpus 3`` without torchrun: the master process plus two helper agent processes
-    (``parallel.agent_process``); the bench process is agent 0. One pod per agent."""
+    """``--gpus 3 --agent0 thread`` without torchrun: the master process plus two helper agent
+    processes (``parallel.agent_process``); the bench process is agent 0. One pod per agent."""
     record = tmp_path / "record"
     env = dict(os.environ, PYTHONPATH=ROOT, SDK_BENCH_RECORD=str(record))
     p = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "3", "--steps", "1", "--warmup", "1",
-                        "--no-gpu-probe", "--allocation-interval", "0.05", "--reference-steps", "1"],
+                        "--no-gpu-probe", "--allocation-interval", "0.05", "--reference-steps", "1",
+                        "--agent0", "thread"],
                        capture_output=True, text=True, timeout=280, env=env, cwd=ROOT)
     assert p.returncode == 0, p.stderr[-3000:]
     recs = _json_lines(p.stdout)

@@ -336,3 +336,19 @@ def test_runtime_reports_running_before_a_check_unless_checks_are_fast(monkeypat
             assert reports == [["starting", "running"], ["ready"]]           # window 0: always RUNNING first
     finally:
         rt.shutdown()
+
+
+def test_ready_returns_what_arrived_without_blocking():
+    a, b = socket.socketpair()
+    try:
+        reader = FrameReader(b)
+        assert reader.ready() == []                       # nothing yet: no wait
+        a.sendall(frame(b"one") + frame(b"two") + frame(b"thr")[:5])
+        time.sleep(0.05)
+        assert reader.ready() == [b"one", b"two"]         # the torn third frame stays buffered
+        a.sendall(frame(b"thr")[5:])
+        a.shutdown(socket.SHUT_WR)
+        assert next(reader.batches()) == [b"thr"]
+    finally:
+        a.close()
+        b.close()
