@@ -509,6 +509,14 @@ class OfferProcessor:
             self._thread.join(timeout=5)
 
     def _loop(self) -> None:
+        prewarm = getattr(self.client, "prewarm", None)
+        if prewarm is not None:
+            # registration to the first offers is a master round trip: build what the first
+            # evaluation would otherwise build meanwhile (never fatal; the evaluation builds it)
+            try:
+                prewarm()
+            except Exception:  # noqa: BLE001
+                LOGGER.debug("offer-evaluation prewarm failed", exc_info=True)
         while not self._stop.is_set():
             try:
                 wait = self.offer_wait_s

@@ -20,10 +20,10 @@ from dcos_commons_amd.mesos import protos as P
 from dcos_commons_amd.offer import task_utils
 from dcos_commons_amd.offer.history import OfferOutcome, OfferOutcomeTracker, OfferOutcomeTrackerV2
 from dcos_commons_amd.offer.resource_pool import MesosResourcePool
-from dcos_commons_amd.offer.resources import get_resource_id
+from dcos_commons_amd.offer.resources import get_resource_id, new_reservation, new_root_volume
 from dcos_commons_amd.offer.taskdata.labels import TaskException, TaskLabelReader
 from dcos_commons_amd.scheduler.plan.pod_instance_requirement import PodInstanceRequirement, RecoveryType
-from dcos_commons_amd.specification.specs import GoalState, NamedVIPSpec, PortSpec, ResourceSpec
+from dcos_commons_amd.specification.specs import GoalState, NamedVIPSpec, PortSpec, ResourceSpec, VolumeType
 from dcos_commons_amd.utils.logging_utils import get_logger
 
 from .outcome import EvaluationOutcome
@@ -238,6 +238,45 @@ class OfferEvaluator:
             self._track(requirement, True, offer, details.render, outcomes)
             return recs
         return []
+
+    def prewarm(self, requirement: PodInstanceRequirement) -> None:
+        """Builds what the first evaluation of a new footprint for ``requirement`` would build
+        before it could match an offer: the pod's PodInfoBuilder template (the other instances
+        are moved from it) and the wire templates of its new reservations and ROOT volumes. The
+        scheduler runs it for its candidate steps between registering and its first offers,
+        which is a master round trip of idle time (``OfferProcessor._loop``); without it the
+        first pod of every deploy pays ~2x the evaluation of the next ones."""
+        fid_proto = self._fid()
+        if self._framework_id is None:
+            self._framework_id = fid_proto.value
+        pi = requirement.pod_instance
+        this_pod = {}
+        for name in task_utils.get_task_names(pi):
+            t = self.state_store.fetch_task_shared(name)
+            if t is not None:
+                this_pod[name] = t
+        if not self._uses_new_pipeline(requirement, this_pod):
+            return      # a relaunch on existing reservations: nothing new is built
+        override_map = {ts.name: self.state_store.fetch_goal_override_status(f"{pi.name}-{ts.name}").target
+                        for ts in pi.pod.tasks}
+        self._template(requirement, self.get_target_config(requirement, this_pod), override_map, fid_proto)
+        ns, fid = self.resource_namespace, self._framework_id
+        tasks = sorted(pi.pod.tasks, key=lambda t: t.name)
+        if not tasks:
+            return
+        first = _ordered_resource_specs(tasks[0].resource_set)
+        specs = list(self._executor_specs_for(first[0].role, first[0].principal, first[0].pre_reserved_role)) \
+            if first else []
+        volumes = list(pi.pod.volumes)
+        for ts in tasks:
+            specs.extend(r for r in ts.resource_set.resources if not isinstance(r, (PortSpec, NamedVIPSpec)))
+            volumes.extend(ts.resource_set.volumes)
+        for spec in specs:
+            new_reservation(spec, ns, fid)
+        for v in volumes:
+            if v.type == VolumeType.ROOT:
+                new_reservation(v, ns, fid)
+                new_root_volume(v, "00000000-0000-4000-8000-000000000000", ns, fid)
 
     def _track(self, requirement, passed, offer, details, outcomes) -> None:
         if self.offer_outcome_tracker is not None:

@@ -195,6 +195,19 @@ class DefaultScheduler(AbstractScheduler):
 
     supports_launch_stream = True
 
+    def prewarm(self) -> None:
+        """Before the first offers: the offer evaluator's templates for the first candidate step
+        of each pod type (``OfferEvaluator.prewarm``)."""
+        seen = set()
+        for step in self.plan_coordinator.get_candidates():
+            if not step.is_pending():
+                continue
+            req = step.get_pod_instance_requirement()
+            if req is None or req.pod_instance.pod.type in seen:
+                continue
+            seen.add(req.pod_instance.pod.type)
+            self.plan_scheduler.offer_evaluator.prewarm(req)
+
     def _record(self, recs) -> bool:
         """Write-ahead: persist the launches before anything is sent to the master."""
         try:
