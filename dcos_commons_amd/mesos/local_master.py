@@ -26,6 +26,7 @@ actions, and scheduler callbacks are delivered from that thread in order.
 """
 from __future__ import annotations
 
+import contextlib
 import heapq
 import itertools
 import logging
@@ -326,6 +327,10 @@ class LocalMaster:
                  clock: Callable[[], float] = time.monotonic):
         self.allocation_interval_s = allocation_interval_s
         self.behavior = behavior or TaskBehavior()
+        # () -> context manager around the delivery of one agent report batch: a network front end
+        # (stream_api.StreamMaster) sets one that writes the batch's events to each framework's
+        # connection in one write, so its scheduler reads them together
+        self.batch_delivery: Callable[[], "contextlib.AbstractContextManager"] = contextlib.nullcontext
         # ProcessTaskBehavior (mesos.containerizer) runs task commands for real
         self._executes = bool(getattr(self.behavior, "executes_commands", False))
         self.domain = domain
@@ -964,6 +969,10 @@ class LocalMaster:
         self._schedule(0, self._apply_runtime_reports, agent_id, list(reports))
 
     def _apply_runtime_reports(self, agent_id: str, reports: List[dict]) -> None:
+        with self.batch_delivery():
+            self._apply_reports(agent_id, reports)
+
+    def _apply_reports(self, agent_id: str, reports: List[dict]) -> None:
         a = self.agents.get(agent_id)
         for r in reports:
             t = a.tasks.get(r.get("task")) if a is not None else None

@@ -198,6 +198,8 @@ class DefaultScheduler(AbstractScheduler):
     def prewarm(self) -> None:
         """Before the first offers: the offer evaluator's templates for the first candidate step
         of each pod type (``OfferEvaluator.prewarm``)."""
+        if not self.scheduler_config.is_offer_prewarm():
+            return
         seen = set()
         for step in self.plan_coordinator.get_candidates():
             if not step.is_pending():

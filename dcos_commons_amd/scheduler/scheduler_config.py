@@ -303,6 +303,11 @@ class SchedulerConfig:
         reference's driver callbacks do). See ``OfferProcessor.wait_cycle_idle``."""
         return self.env.get_optional_double("SDK_STATUS_CYCLE_WAIT_MS", 100.0) / 1000.0
 
+    def is_offer_prewarm(self) -> bool:
+        """Build the first evaluation's templates between registration and the first offers
+        (``SDK_OFFER_PREWARM``; ``DefaultScheduler.prewarm``)."""
+        return self.env.get_optional_boolean("SDK_OFFER_PREWARM", True)
+
     def offer_hold_s(self) -> float:
         """Hold unused offers this long while WORKING instead of declining them for 1 h
         (0 = reference behaviour: long decline + rate-limited revive)."""

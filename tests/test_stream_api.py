@@ -352,3 +352,30 @@ def test_ready_returns_what_arrived_without_blocking():
     finally:
         a.close()
         b.close()
+
+
+def test_corked_events_leave_in_one_write_per_connection():
+    from dcos_commons_amd.mesos.stream_api import _StreamSubscription, corked
+
+    a, b = socket.socketpair()
+    c, d = socket.socketpair()
+    try:
+        s1, s2 = _StreamSubscription(a, 15.0), _StreamSubscription(c, 15.0)
+        writes = []
+        for s in (s1, s2):
+            orig = s.write
+            s.write = lambda data, orig=orig, s=s: (writes.append((s, len(data))), orig(data))
+        ev = P.Event(type=P.Event.HEARTBEAT)
+        with corked():
+            s1.put(ev)
+            s2.put(ev)
+            with corked():          # nested blocks write with the outermost
+                s1.put(ev)
+            assert writes == []
+        assert sorted((id(s), n) for s, n in writes) == sorted([(id(s1), 2 * len(frame(ev.SerializeToString()))),
+                                                              (id(s2), len(frame(ev.SerializeToString())))])
+        s1.put(ev)                  # uncorked: written at once
+        assert len(writes) == 3
+    finally:
+        for x in (a, b, c, d):
+            x.close()
