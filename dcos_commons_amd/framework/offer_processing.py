@@ -512,9 +512,14 @@ class OfferProcessor:
         prewarm = getattr(self.client, "prewarm", None)
         if prewarm is not None:
             # registration to the first offers is a master round trip: build what the first
-            # evaluation would otherwise build meanwhile (never fatal; the evaluation builds it)
+            # evaluation would otherwise build meanwhile, in steps that give the interpreter to the
+            # event thread and stop once offers are queued (never fatal: the evaluation builds
+            # whatever is missing)
+            def stop() -> bool:
+                time.sleep(0)
+                return self._stop.is_set() or not self.queue.is_empty()
             try:
-                prewarm()
+                prewarm(stop)
             except Exception:  # noqa: BLE001
                 LOGGER.debug("offer-evaluation prewarm failed", exc_info=True)
         while not self._stop.is_set():

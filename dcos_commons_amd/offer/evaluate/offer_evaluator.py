@@ -239,13 +239,14 @@ class OfferEvaluator:
             return recs
         return []
 
-    def prewarm(self, requirement: PodInstanceRequirement) -> None:
+    def prewarm(self, requirement: PodInstanceRequirement, stop=lambda: False) -> bool:
         """Builds what the first evaluation of a new footprint for ``requirement`` would build
         before it could match an offer: the pod's PodInfoBuilder template (the other instances
         are moved from it) and the wire templates of its new reservations and ROOT volumes. The
         scheduler runs it for its candidate steps between registering and its first offers,
         which is a master round trip of idle time (``OfferProcessor._loop``); without it the
-        first pod of every deploy pays ~2x the evaluation of the next ones."""
+        first pod of every deploy pays ~2x the evaluation of the next ones. ``stop()`` is asked
+        between the pieces; False when it ended the prewarm early."""
         fid_proto = self._fid()
         if self._framework_id is None:
             self._framework_id = fid_proto.value
@@ -256,14 +257,14 @@ class OfferEvaluator:
             if t is not None:
                 this_pod[name] = t
         if not self._uses_new_pipeline(requirement, this_pod):
-            return      # a relaunch on existing reservations: nothing new is built
+            return True     # a relaunch on existing reservations: nothing new is built
         override_map = {ts.name: self.state_store.fetch_goal_override_status(f"{pi.name}-{ts.name}").target
                         for ts in pi.pod.tasks}
         self._template(requirement, self.get_target_config(requirement, this_pod), override_map, fid_proto)
         ns, fid = self.resource_namespace, self._framework_id
         tasks = sorted(pi.pod.tasks, key=lambda t: t.name)
         if not tasks:
-            return
+            return True
         first = _ordered_resource_specs(tasks[0].resource_set)
         specs = list(self._executor_specs_for(first[0].role, first[0].principal, first[0].pre_reserved_role)) \
             if first else []
@@ -272,11 +273,16 @@ class OfferEvaluator:
             specs.extend(r for r in ts.resource_set.resources if not isinstance(r, (PortSpec, NamedVIPSpec)))
             volumes.extend(ts.resource_set.volumes)
         for spec in specs:
+            if stop():
+                return False
             new_reservation(spec, ns, fid)
         for v in volumes:
             if v.type == VolumeType.ROOT:
+                if stop():
+                    return False
                 new_reservation(v, ns, fid)
                 new_root_volume(v, "00000000-0000-4000-8000-000000000000", ns, fid)
+        return True
 
     def _track(self, requirement, passed, offer, details, outcomes) -> None:
         if self.offer_outcome_tracker is not None:

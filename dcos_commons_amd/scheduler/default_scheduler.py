@@ -195,10 +195,10 @@ class DefaultScheduler(AbstractScheduler):
 
     supports_launch_stream = True
 
-    def prewarm(self) -> None:
+    def prewarm(self, stop=lambda: False) -> None:
         """Before the first offers: the offer evaluator's templates for the first candidate step
-        of each pod type (``OfferEvaluator.prewarm``)."""
-        if not self.scheduler_config.is_offer_prewarm():
+        of each pod type (``OfferEvaluator.prewarm``), until ``stop()``."""
+        if not self.scheduler_config.is_offer_prewarm() or stop():
             return
         seen = set()
         for step in self.plan_coordinator.get_candidates():
@@ -208,7 +208,8 @@ class DefaultScheduler(AbstractScheduler):
             if req is None or req.pod_instance.pod.type in seen:
                 continue
             seen.add(req.pod_instance.pod.type)
-            self.plan_scheduler.offer_evaluator.prewarm(req)
+            if stop() or not self.plan_scheduler.offer_evaluator.prewarm(req, stop):
+                return
 
     def _record(self, recs) -> bool:
         """Write-ahead: persist the launches before anything is sent to the master."""

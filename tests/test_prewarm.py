@@ -91,3 +91,25 @@ def test_prewarm_is_idempotent_and_fails_only_quietly():
     except RuntimeError:
         raised = True
     assert raised
+
+
+def test_prewarm_stops_when_offers_are_queued(monkeypatch):
+    """The offer thread's ``stop()`` turns true once offers are queued: the prewarm builds
+    nothing more and the cycle starts."""
+    sched = _scheduler("fw-stop")
+    builds = []
+    orig = PIB.PodInfoBuilder.__init__
+
+    def count(self, *a, **k):
+        builds.append(1)
+        orig(self, *a, **k)
+    monkeypatch.setattr(PIB.PodInfoBuilder, "__init__", count)
+    sched.prewarm(lambda: True)
+    assert builds == []
+    asked = []
+
+    def after_template():           # let the template through, stop before the reservations
+        asked.append(1)
+        return len(asked) > 2
+    sched.prewarm(after_template)
+    assert builds == [1]
