@@ -305,8 +305,10 @@ class SchedulerConfig:
 
     def is_offer_prewarm(self) -> bool:
         """Build the first evaluation's templates between registration and the first offers
-        (``SDK_OFFER_PREWARM``; ``DefaultScheduler.prewarm``)."""
-        return self.env.get_optional_boolean("SDK_OFFER_PREWARM", True)
+        (``SDK_OFFER_PREWARM``; ``DefaultScheduler.prewarm``). Off by default: on the box it took
+        the first evaluation 0.55 -> 0.37 ms but delayed handling the first offers by more, 1 pod
+        2.02 -> 2.27 ms (profiles/prewarm_window_ab_r06_box.txt)."""
+        return self.env.get_optional_boolean("SDK_OFFER_PREWARM", False)
 
     def offer_hold_s(self) -> float:
         """Hold unused offers this long while WORKING instead of declining them for 1 h

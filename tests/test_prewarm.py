@@ -32,7 +32,7 @@ def _offer(i):
 
 def _scheduler(fid):
     env = helloworld_env(2, 1, "true")
-    cfg = SchedulerConfig.for_testing(PORT_API="0")
+    cfg = SchedulerConfig.for_testing(PORT_API="0", SDK_OFFER_PREWARM="true")
     raw = RawServiceSpec.new_builder(os.path.join(SPECS, "gpu.yml")).set_env(env).build()
     spec = ServiceSpecGenerator(raw, cfg, SPECS, env).build()
     sched = SchedulerBuilder(spec, cfg, MemPersister()).set_plans_from(raw).build()
@@ -81,7 +81,7 @@ def test_prewarm_is_idempotent_and_fails_only_quietly():
     # before a framework ID is stored the evaluator cannot build anything: prewarm raises, and
     # the offer thread (OfferProcessor._loop) logs that at debug level and goes on
     env = helloworld_env(1, 1, "true")
-    cfg = SchedulerConfig.for_testing(PORT_API="0")
+    cfg = SchedulerConfig.for_testing(PORT_API="0", SDK_OFFER_PREWARM="true")
     raw = RawServiceSpec.new_builder(os.path.join(SPECS, "gpu.yml")).set_env(env).build()
     spec = ServiceSpecGenerator(raw, cfg, SPECS, env).build()
     fresh = SchedulerBuilder(spec, cfg, MemPersister()).set_plans_from(raw).build()
@@ -113,3 +113,12 @@ def test_prewarm_stops_when_offers_are_queued(monkeypatch):
         return len(asked) > 2
     sched.prewarm(after_template)
     assert builds == [1]
+
+
+def test_prewarm_is_off_by_default(monkeypatch):
+    env = helloworld_env(1, 1, "true")
+    cfg = SchedulerConfig.for_testing(PORT_API="0")
+    raw = RawServiceSpec.new_builder(os.path.join(SPECS, "gpu.yml")).set_env(env).build()
+    spec = ServiceSpecGenerator(raw, cfg, SPECS, env).build()
+    sched = SchedulerBuilder(spec, cfg, MemPersister()).set_plans_from(raw).build()
+    sched.prewarm()         # returns before touching anything (no framework ID needed)

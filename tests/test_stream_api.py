@@ -326,14 +326,14 @@ def test_runtime_reports_running_before_a_check_unless_checks_are_fast(monkeypat
         assert launch("t4") == [["starting", "running"], ["ready"]]          # after a slow check: RUNNING first
     finally:
         rt.shutdown()
-    monkeypatch.setenv("SDK_AGENT_REPORT_WINDOW_MS", "0")
+    monkeypatch.delenv("SDK_AGENT_REPORT_WINDOW_MS")       # the default: RUNNING always first
     rt = AgentRuntime(lambda reps: reports.append([r["event"] for r in reps]), lambda d: True)
     try:
         for tid in ("a", "b"):
             reports.clear()
             rt.handle({"op": "launch", "task": tid, "name": tid, "devices": [0], "check": {"delay": 0, "interval": 1},
                        "timing": {}})
-            assert reports == [["starting", "running"], ["ready"]]           # window 0: always RUNNING first
+            assert reports == [["starting", "running"], ["ready"]]
     finally:
         rt.shutdown()
 
