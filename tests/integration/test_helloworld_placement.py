@@ -262,3 +262,79 @@ def test_region_config_update_does_not_succeed():
             assert _pod_region(pod) == LOCAL_REGION
     finally:
         sdk_install.uninstall(config.PACKAGE_NAME, config.SERVICE_NAME)
+
+
+# -- a changed placement constraint (reference test_placement.py:399-470) ----------------------
+def _task_host(task_name):
+    """The agent a task runs on, from its TaskInfo's offer_hostname label, checked against the
+    task summary (reference ``get_task_host``)."""
+    info = sdk_cmd.service_request("GET", config.SERVICE_NAME, f"/v1/pod/{task_name.rsplit('-', 1)[0]}/info").json()
+    task = next(i["info"] for i in info if i["info"]["name"] == task_name)
+    host = next(lb["value"] for lb in task["labels"]["labels"] if lb["key"] == "offer_hostname")
+    summary = [t for t in sdk_tasks.get_service_tasks(config.SERVICE_NAME) if t.name == task_name]
+    assert len(summary) == 1 and summary[0].host == host, (host, summary)
+    return host
+
+
+def _setup_constraint_switch():
+    """hello-0 pinned to one agent, then the service's placement switched to another agent."""
+    some_agent, other_agent = _local_agents()[:2]
+    sdk_install.install(config.PACKAGE_NAME, config.SERVICE_NAME, 1, additional_options={
+        "service": {"yaml": "marathon_constraint"},
+        "hello": {"count": 1, "placement": f'[["hostname", "LIKE", "{some_agent}"]]'},
+        "world": {"count": 0}})
+    old_ids = sdk_tasks.get_task_ids(config.SERVICE_NAME, "hello")
+    app = sdk_marathon.get_config(config.SERVICE_NAME)
+    app["env"]["HELLO_PLACEMENT"] = f'[["hostname", "LIKE", "{other_agent}"]]'
+    sdk_marathon.update_app(app)
+    sdk_plan.wait_for_completed_deployment(config.SERVICE_NAME)
+    return some_agent, other_agent, old_ids
+
+
+def test_updated_placement_constraints_no_task_change():
+    """A placement change alone is not a task change: nothing relaunches or moves."""
+    some_agent, _, old_ids = _setup_constraint_switch()
+    try:
+        sdk_tasks.check_tasks_not_updated(config.SERVICE_NAME, "hello", old_ids)
+        assert _task_host("hello-0-server") == some_agent
+    finally:
+        sdk_install.uninstall(config.PACKAGE_NAME, config.SERVICE_NAME)
+
+
+def test_updated_placement_constraints_not_applied_with_other_changes():
+    """A new pod follows the new constraint; the running one stays where it is."""
+    some_agent, other_agent, _ = _setup_constraint_switch()
+    try:
+        app = sdk_marathon.get_config(config.SERVICE_NAME)
+        app["env"]["HELLO_COUNT"] = "2"
+        sdk_marathon.update_app(app)
+        sdk_tasks.check_running(config.SERVICE_NAME, 2)
+        sdk_plan.wait_for_completed_deployment(config.SERVICE_NAME)
+        assert _task_host("hello-0-server") == some_agent
+        assert _task_host("hello-1-server") == other_agent
+    finally:
+        sdk_install.uninstall(config.PACKAGE_NAME, config.SERVICE_NAME)
+
+
+def test_updated_placement_constraints_restarted_tasks_dont_move():
+    """A restart relaunches in place, on the pod's reservations, whatever the constraint says."""
+    some_agent, _, old_ids = _setup_constraint_switch()
+    try:
+        sdk_cmd.svc_cli(config.PACKAGE_NAME, config.SERVICE_NAME, "pod restart hello-0")
+        sdk_tasks.check_tasks_updated(config.SERVICE_NAME, "hello", old_ids)
+        sdk_plan.wait_for_completed_recovery(config.SERVICE_NAME)
+        assert _task_host("hello-0-server") == some_agent
+    finally:
+        sdk_install.uninstall(config.PACKAGE_NAME, config.SERVICE_NAME)
+
+
+def test_updated_placement_constraints_replaced_tasks_do_move():
+    """A replace is a new footprint: it is placed by the new constraint."""
+    _, other_agent, old_ids = _setup_constraint_switch()
+    try:
+        sdk_cmd.svc_cli(config.PACKAGE_NAME, config.SERVICE_NAME, "pod replace hello-0")
+        sdk_tasks.check_tasks_updated(config.SERVICE_NAME, "hello", old_ids)
+        sdk_plan.wait_for_completed_recovery(config.SERVICE_NAME)
+        assert _task_host("hello-0-server") == other_agent
+    finally:
+        sdk_install.uninstall(config.PACKAGE_NAME, config.SERVICE_NAME)
