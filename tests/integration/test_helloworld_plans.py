@@ -1,7 +1,7 @@
 """Plan and goal-state scenarios on the local cluster.
 
-Reference: frameworks/helloworld/tests/{test_goal_states.py, test_multistep_plan.py,
-test_custom_plan.py, test_sidecar.py, test_uninstall.py, test_decommission.py}. Each scenario
+Reference: frameworks/helloworld/tests/{test_multistep_plan.py,
+test_custom_plan.py, test_uninstall.py, test_decommission.py}. Each scenario
 installs its own service from one of the helloworld specs, drives it with the CLI / HTTP API the
 way an operator would, and checks what really ran in the task sandboxes.
 """
@@ -17,33 +17,6 @@ pytestmark = pytest.mark.usefixtures("local_cluster")
 
 def completed_ids(task_name):
     return [t.id for t in sdk_tasks.get_summary(with_completed=True, task_name=task_name) if t.is_completed]
-
-
-def test_goal_states_once_and_finish():
-    svc = "/test/integration/hello-goals"
-    sdk_install.install(PKG, svc, 3, additional_options={"service": {"yaml": "finish_state"}})
-    try:
-        sdk_plan.wait_for_completed_deployment(svc)
-        once = completed_ids("hello-0-once")
-        init = completed_ids("world-0-init")
-        assert len(once) == 1 and len(init) == 1
-        rc, out, _ = sdk_cmd.service_task_exec(svc, "world-0-server", "true")
-        assert rc == 0
-
-        # ONCE: a config update of its pod relaunches the server, never the one-shot task
-        hello_server = sdk_tasks.get_task_ids(svc, "hello-0-server")
-        config.bump_hello_cpus(svc)
-        sdk_tasks.check_tasks_updated(svc, "hello-0-server", hello_server)
-        sdk_tasks.check_task_not_relaunched(svc, "hello-0-once", once[0], with_completed=True)
-
-        # FINISH: it reruns (and finishes again) whenever its pod's config changes
-        config.bump_world_cpus(svc)
-        sdk_tasks.check_task_relaunched("world-0-init", init[0], ensure_new_task_not_completed=False)
-        sdk_plan.wait_for_completed_deployment(svc)
-        assert len(completed_ids("world-0-init")) == 2
-        config.check_running(svc)
-    finally:
-        sdk_install.uninstall(PKG, svc)
 
 
 def test_multistep_plan_shared_resource_set():
@@ -71,42 +44,6 @@ def test_custom_plan_scenario_reverses_steps():
         plan = sdk_plan.get_deployment_plan(svc)
         world_steps = plan["phases"][1]["steps"]
         assert [s["name"] for s in world_steps] == ["world-1:[server]", "world-0:[server]"]
-    finally:
-        sdk_install.uninstall(PKG, svc)
-
-
-@needs_cli
-def test_sidecar_plan_runs_one_shot_tasks_against_the_pod_volume():
-    svc = "hello-sidecar"
-    sdk_install.install(PKG, svc, 2, additional_options={"service": {"yaml": "sidecar"}, "hello": {"count": 2}})
-    try:
-        servers = sdk_tasks.get_task_ids(svc, "")
-        rc, _, err = sdk_cmd.svc_cli(PKG, svc, "plan start sidecar -p BACKUP_TAG=t1")
-        assert rc == 0, err
-        sdk_plan.wait_for_completed_plan(svc, "sidecar")
-        # backup then verify ran once per pod, in the pod's executor, on the shared ROOT volume
-        for i in (0, 1):
-            assert len(completed_ids(f"hello-{i}-backup")) == 1
-            assert len(completed_ids(f"hello-{i}-verify")) == 1
-            rc, out, _ = sdk_cmd.service_task_exec(svc, f"hello-{i}-server",
-                                                   "test -f shared-data/backup.tgz && cat shared-data/backup-tag")
-            assert rc == 0 and out.strip() == "t1"     # the plan parameter reached the sidecar
-        sdk_tasks.check_tasks_not_updated(svc, "hello", servers)
-        # a second run is a new launch of the one-shot tasks
-        assert sdk_cmd.svc_cli(PKG, svc, "plan start sidecar")[0] == 0
-        sdk_plan._poll(lambda: len(completed_ids("hello-0-verify")) == 2, 60, "second sidecar run")
-        sdk_plan.wait_for_completed_plan(svc, "sidecar")
-
-        # a failing ONCE task never triggers recovery, not even after a scheduler restart
-        assert sdk_plan.get_plan(svc, "recovery")["status"] == "COMPLETE"
-        sdk_plan.start_plan(svc, "sidecar-toxic")
-        sdk_plan._poll(lambda: sdk_cmd.service_task_exec(svc, "hello-0-server", "cat shared-data/toxic-output")[1]
-                       .strip().startswith("toxic"), 60, "toxic sidecar ran")
-        sdk_marathon.restart_app(svc)
-        sdk_plan.wait_for_completed_deployment(svc)
-        recovery = sdk_plan.get_plan(svc, "recovery")
-        assert recovery["status"] == "COMPLETE" and recovery["phases"] == []
-        sdk_tasks.check_tasks_not_updated(svc, "hello", servers)
     finally:
         sdk_install.uninstall(PKG, svc)
 
