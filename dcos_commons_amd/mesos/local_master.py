@@ -311,6 +311,8 @@ class _Framework:
     # agent id -> [(expiry, declined resources)]: Mesos' RefusedOfferFilter -- an agent's offer is
     # filtered only while everything it would contain is within a declined set
     filters: Dict[str, list] = field(default_factory=dict)
+    # which of a MULTI_ROLE framework's roles gets the next agent's unreserved resources
+    rr: int = 0
 
 
 @dataclass
@@ -695,9 +697,13 @@ class LocalMaster:
     def _alloc_role(fw: _Framework, role: str) -> Optional[str]:
         """The framework role that may be allocated a resource reserved for ``role``: the role
         itself, or (hierarchical roles) a sub-role of it, which can then refine the reservation
-        (``slave_public`` resources go to a framework subscribed as ``slave_public/<svc>-role``)."""
+        (``slave_public`` resources go to a framework subscribed as ``slave_public/<svc>-role``).
+        Unreserved resources go to the framework's top-level roles in turn, one agent's offer at
+        a time (``fw.rr``), as Mesos' allocator spreads them over a MULTI_ROLE framework's roles:
+        a service migrating between its legacy and its group role gets offers for both."""
         if role == "*":
-            return sorted(fw.roles)[0]
+            tops = sorted(r for r in fw.roles if "/" not in r) or sorted(fw.roles)
+            return tops[getattr(fw, "rr", 0) % len(tops)]
         if role in fw.roles:
             return role
         return next((r for r in sorted(fw.roles) if r.startswith(role + "/")), None)
@@ -725,6 +731,7 @@ class LocalMaster:
                     a.available.subtract(r)
                 for r in mine:
                     r.allocation_info.role = self._alloc_role(fw, effective_role(r))
+                fw.rr += 1
                 oid = "offer-" + ids.uuid4_hex()
                 self.offers[oid] = _Offer(oid, fw.id, a.id, mine)
                 o = P.Offer(hostname=a.spec.hostname)

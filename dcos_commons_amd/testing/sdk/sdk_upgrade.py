@@ -86,7 +86,9 @@ def test_upgrade(package_name: str, service_name: str, expected_running_tasks: i
 
 
 def test_downgrade(package_name: str, service_name: str, expected_running_tasks: int,
-                   timeout_seconds: int = TIMEOUT_SECONDS) -> None:
+                   timeout_seconds: int = TIMEOUT_SECONDS, to_options: Optional[Dict[str, Any]] = None) -> None:
+    """To the oldest registered version (the reference's ``to_version``: its previous release),
+    with ``to_options`` if given."""
     versions = _cosmos().versions(package_name)
-    update_or_upgrade_or_downgrade(package_name, service_name, versions[0], {}, expected_running_tasks,
+    update_or_upgrade_or_downgrade(package_name, service_name, versions[0], to_options or {}, expected_running_tasks,
                                    True, timeout_seconds)

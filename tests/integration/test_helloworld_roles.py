@@ -1,14 +1,12 @@
 """helloworld role scenarios on the local cluster: quota groups, role migration, pre-reserved roles.
 
-Reference: frameworks/helloworld/tests/{test_quota_deployment.py, test_quota_upgrade.py,
-test_quota_downgrade.py, test_pre_reserved_sidecar.py, test_resource_refinement.py}.
+Reference: frameworks/helloworld/tests/{test_quota_deployment.py, test_pre_reserved_sidecar.py,
+test_resource_refinement.py}; the upgrade and downgrade sequences are
+test_helloworld_quota_{upgrade,downgrade}.py.
 
 * Marathon groups decide the scheduler's role: a group with ``enforceRole`` makes its name the
   role of every service under it; without it a service keeps its legacy ``<name>-role`` unless
   it asks for the group role, and ``enable_role_migration`` subscribes with both roles.
-* Migration: a legacy-role service updated to the group role with migration on keeps its pods on
-  the legacy role until each pod is replaced; new pods land on the group role; turning migration
-  off leaves a single-role framework.
 * Pre-reserved roles: pods with ``pre-reserved-role: slave_public`` refine the statically reserved
   resources of every agent, a sidecar plan runs on them, and another framework's persistent volume
   on the same static reservation survives the service's install and uninstall.
@@ -115,58 +113,6 @@ def test_non_migration(quota_group, enforce_role):
         {"service": {"name": SERVICE_NAME, "role": ENFORCED_ROLE, "enable_role_migration": False}})
     assert LEGACY_ROLE not in task_roles.values() and ENFORCED_ROLE in task_roles.values()
     assert roles["framework-roles"] is None and roles["framework-role"] == ENFORCED_ROLE
-
-
-# -- quota upgrade: legacy role -> group role ------------------------------------------------------
-def test_legacy_to_group_role_migration(quota_group):
-    sdk_marathon.create_group(group_id=ENFORCED_ROLE, options={"enforceRole": False})
-    roles, task_roles = _install_and_fetch_service_roles({"service": {"name": SERVICE_NAME}})
-    assert set(task_roles.values()) == {LEGACY_ROLE} and roles["framework-role"] == LEGACY_ROLE
-
-    # the scheduler moves to the group role and subscribes with both roles; pods stay put
-    sdk_upgrade.update_or_upgrade_or_downgrade(
-        config.PACKAGE_NAME, SERVICE_NAME, to_version=None, expected_running_tasks=3,
-        to_options={"service": {"name": SERVICE_NAME, "role": ENFORCED_ROLE, "enable_role_migration": True}})
-    roles = sdk_utils.get_service_roles(SERVICE_NAME)
-    assert set(roles["task-roles"].values()) == {LEGACY_ROLE}
-    assert roles["framework-role"] is None and sorted(roles["framework-roles"]) == sorted([LEGACY_ROLE, ENFORCED_ROLE])
-
-    # replacing a pod re-reserves it under the group role
-    for pod in ("hello-0", "world-0", "world-1"):
-        old_ids = sdk_tasks.get_task_ids(SERVICE_NAME, pod)
-        rc, _, _ = sdk_cmd.svc_cli(config.PACKAGE_NAME, SERVICE_NAME, f"pod replace {pod}")
-        assert rc == 0
-        # (the recovery completes within milliseconds here: wait on the relaunch, not on the plan
-        # being seen IN_PROGRESS)
-        sdk_tasks.check_tasks_updated(SERVICE_NAME, pod, old_ids)
-        sdk_plan.wait_for_completed_recovery(SERVICE_NAME)
-
-        @sdk_utils.retry(timeout_s=30, interval_s=0.2)
-        def moved():
-            assert sdk_utils.get_service_roles(SERVICE_NAME)["task-roles"][f"{pod}-server"] == ENFORCED_ROLE
-        moved()
-    roles = sdk_utils.get_service_roles(SERVICE_NAME)
-    assert set(roles["task-roles"].values()) == {ENFORCED_ROLE}
-    # the legacy reservations were released
-    assert not sdk_install._cluster().reserved_resources(LEGACY_ROLE)
-
-    # new pods land on the group role
-    cfg = sdk_marathon.get_config(SERVICE_NAME)
-    cfg["env"]["HELLO_COUNT"], cfg["env"]["WORLD_COUNT"] = "2", "3"
-    sdk_marathon.update_app(cfg)
-    sdk_plan.wait_for_completed_deployment(SERVICE_NAME)
-    sdk_tasks.check_running(SERVICE_NAME, 5)
-    roles = sdk_utils.get_service_roles(SERVICE_NAME)
-    assert len(roles["task-roles"]) == 5 and set(roles["task-roles"].values()) == {ENFORCED_ROLE}
-
-    # migration off: a single-role framework on the group role
-    sdk_upgrade.update_or_upgrade_or_downgrade(
-        config.PACKAGE_NAME, SERVICE_NAME, to_version=None, expected_running_tasks=5,
-        to_options={"service": {"name": SERVICE_NAME, "role": ENFORCED_ROLE, "enable_role_migration": False},
-                    "hello": {"count": 2}, "world": {"count": 3}})
-    roles = sdk_utils.get_service_roles(SERVICE_NAME)
-    assert roles["framework-roles"] is None and roles["framework-role"] == ENFORCED_ROLE
-    assert set(roles["task-roles"].values()) == {ENFORCED_ROLE}
 
 
 # -- pre-reserved roles --------------------------------------------------------------------------
