@@ -14,8 +14,8 @@ from dcos_commons_amd.testing.sdk import sdk_cmd, sdk_install, sdk_plan, sdk_tas
 from tests.integration import hw_config as config
 from tests.integration.conftest import make_cluster, needs_cli
 
-# every agent: one plain 2 GB disk and one 1 GB disk of the "fast-nvme" profile
-MOUNT_DISKS = (("/dcos/volume0", 2000.0), ("/dcos/volume1", 1000.0, "fast-nvme"))
+# every agent: two plain 2 GB disks and one 1 GB disk of the "fast-nvme" profile
+MOUNT_DISKS = (("/dcos/volume0", 2000.0), ("/dcos/volume1", 1000.0, "fast-nvme"), ("/dcos/volume2", 2000.0))
 
 
 @pytest.fixture(scope="module")
@@ -108,29 +108,66 @@ def test_host_volume_mounts():
         sdk_install.uninstall(config.PACKAGE_NAME, config.SERVICE_NAME)
 
 
-@needs_cli
-def test_pod_mount_volume_survives_task_kill():
-    sdk_install.install(config.PACKAGE_NAME, config.SERVICE_NAME, 2,
+@pytest.fixture
+def pod_mount_service():
+    sdk_install.install(config.PACKAGE_NAME, config.SERVICE_NAME, 4,
                         additional_options={"service": {"yaml": "pod-mount-volume"}, "hello": {"count": 2}})
-    try:
-        rc, out, _ = sdk_cmd.svc_cli(config.PACKAGE_NAME, config.SERVICE_NAME, "pod info hello-0", print_output=False)
-        assert rc == 0
-        task = json.loads(out)[0]["info"]
-        (path, pid, size, source), = _volumes(task)
-        # the whole plain disk, not the profiled one
-        assert path == "mount-data" and size == 2000.0
-        assert source["type"] == "MOUNT" and source["mount"]["root"] == "/dcos/volume0" and "profile" not in source
-        old = sdk_tasks.get_service_tasks(config.SERVICE_NAME, "hello-0-server")[0]
-        sdk_cmd.service_task_exec(config.SERVICE_NAME, "hello-0-server", "echo kept > mount-data/marker")
-        assert sdk_cmd.kill_task_with_pattern("df mount-data", agent_host=old.host)
-        sdk_tasks.check_task_relaunched("hello-0-server", old.id)
-        sdk_plan.wait_for_completed_recovery(config.SERVICE_NAME)
-        rc, out, _ = sdk_cmd.svc_cli(config.PACKAGE_NAME, config.SERVICE_NAME, "pod info hello-0", print_output=False)
-        assert _volumes(json.loads(out)[0]["info"])[0][1] == pid
-        rc, out, _ = sdk_cmd.service_task_exec(config.SERVICE_NAME, "hello-0-server", "cat mount-data/marker")
-        assert rc == 0 and out.strip() == "kept"
-    finally:
-        sdk_install.uninstall(config.PACKAGE_NAME, config.SERVICE_NAME)
+    yield
+    sdk_install.uninstall(config.PACKAGE_NAME, config.SERVICE_NAME)
+
+
+def _verify_shared_executor(pod):
+    """Both tasks of ``pod`` run in one executor and see each other's writes to the pod volume
+    (reference test_mount_volumes.py ``verify_shared_executor``)."""
+    infos = [t["info"] for t in _pod_info(pod)]
+    assert len(infos) == 2
+    assert infos[0]["executor"] == infos[1]["executor"]
+    rc, out, _ = sdk_cmd.service_task_exec(config.SERVICE_NAME, f"{pod}-agent", "sort -u mount-data/written-by")
+    assert rc == 0 and out.split() == ["agent", "node"], out
+
+
+@needs_cli
+def test_pod_mount_volume_survives_task_kill(pod_mount_service):
+    rc, out, _ = sdk_cmd.svc_cli(config.PACKAGE_NAME, config.SERVICE_NAME, "pod info hello-0", print_output=False)
+    assert rc == 0
+    infos = {i["info"]["name"]: i["info"] for i in json.loads(out)}
+    pod_vol = [v for v in _volumes(infos["hello-0-node"]) if v[0] == "mount-data"]
+    node_vol = [v for v in _volumes(infos["hello-0-node"]) if v[0] == "node-disk"]
+    (_, pid, size, source), = pod_vol
+    # whole plain disks, never the profiled one; the node task's own disk is the other plain one
+    assert size == 2000.0 and source["type"] == "MOUNT" and "profile" not in source
+    assert node_vol[0][3]["mount"]["root"] != source["mount"]["root"] and "profile" not in node_vol[0][3]
+    old = sdk_tasks.get_service_tasks(config.SERVICE_NAME, "hello-0-node")[0]
+    sdk_cmd.service_task_exec(config.SERVICE_NAME, "hello-0-node", "echo kept > mount-data/marker")
+    assert sdk_cmd.kill_task_with_pattern("df mount-data", agent_host=old.host)
+    sdk_tasks.check_task_relaunched("hello-0-node", old.id)
+    sdk_plan.wait_for_completed_recovery(config.SERVICE_NAME)
+    relaunched = {i["info"]["name"]: i["info"] for i in _pod_info("hello-0")}
+    assert [v[1] for v in _volumes(relaunched["hello-0-node"]) if v[0] == "mount-data"] == [pid]
+    rc, out, _ = sdk_cmd.service_task_exec(config.SERVICE_NAME, "hello-0-node", "cat mount-data/marker")
+    assert rc == 0 and out.strip() == "kept"
+
+
+def _kill_one(pod, victim, survivor, pattern):
+    _verify_shared_executor(pod)
+    tasks = {t.name: t for t in sdk_tasks.get_service_tasks(config.SERVICE_NAME, pod)}
+    assert set(tasks) == {f"{pod}-node", f"{pod}-agent"}
+    assert sdk_cmd.kill_task_with_pattern(pattern, agent_host=tasks[f"{pod}-{victim}"].host)
+    sdk_tasks.check_tasks_updated(config.SERVICE_NAME, f"{pod}-{victim}", [tasks[f"{pod}-{victim}"].id])
+    sdk_plan.wait_for_completed_recovery(config.SERVICE_NAME)
+    sdk_tasks.check_tasks_not_updated(config.SERVICE_NAME, f"{pod}-{survivor}", [tasks[f"{pod}-{survivor}"].id])
+    # the relaunch ran in the same executor, against the same pod volume
+    _verify_shared_executor(pod)
+
+
+def test_kill_node(pod_mount_service):
+    """Kill the node task: only it is relaunched, in the pod's running executor."""
+    _kill_one("hello-0", "node", "agent", "node-disk/written-by")
+
+
+def test_kill_agent(pod_mount_service):
+    """Kill the agent task: only it is relaunched, in the pod's running executor."""
+    _kill_one("hello-0", "agent", "node", "agent-root/written-by")
 
 
 def test_profile_mount_volume():
@@ -151,10 +188,10 @@ def test_testing_volumes_added_to_running_agents(local_cluster):
     from dcos_commons_amd.tools.create_testing_volumes import create_testing_volumes
 
     roots = create_testing_volumes(local_cluster, count=1, size_mb=300.0, profile="xfs")
-    assert roots and all(r == "/dcos/volume2" for r in roots)   # after the module's two disks
+    assert roots and all(r == "/dcos/volume3" for r in roots)   # after the module's three disks
     for aid in local_cluster.agent_ids.values():
         offered = [r for r in local_cluster.master.agent_resources(aid)
-                   if r.HasField("disk") and r.disk.source.mount.root == "/dcos/volume2"]
+                   if r.HasField("disk") and r.disk.source.mount.root == "/dcos/volume3"]
         assert len(offered) == 1 and offered[0].disk.source.profile == "xfs" and offered[0].scalar.value == 300.0
     sdk_install.install(config.PACKAGE_NAME, config.SERVICE_NAME, 1, additional_options={
         "service": {"yaml": "profile-mount-volume"}})

@@ -161,8 +161,11 @@ def test_gpu_and_mount_volumes():
     _run("gpu_resource.yml", gpus)
 
     def mount(sim):
-        disks = [r for r in _executor(sim, "hello-0-server").resources if r.name == "disk"]
+        disks = [r for r in _executor(sim, "hello-0-node").resources if r.name == "disk"]
         assert disks and disks[0].disk.source.type == P.Resource.DiskInfo.Source.MOUNT
+        own = {t: [r.disk.source.type for r in _launched(sim)[f"hello-0-{t}"].resources if r.name == "disk"]
+               for t in ("node", "agent")}
+        assert own["node"] == [P.Resource.DiskInfo.Source.MOUNT] and own["agent"] == [0]   # 0: no source, ROOT
     _run("pod-mount-volume.yml", mount)
 
 
