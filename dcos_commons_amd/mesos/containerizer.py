@@ -410,6 +410,9 @@ class ProcessTaskBehavior(TaskBehavior):
         self.artifact_resolver = artifact_resolver
         self.default_kill_grace_s = default_kill_grace_s
         self.extra_env = dict(extra_env or {})
+        # the cluster's metrics service (testing.cluster.metrics.LocalMetrics): each task gets the
+        # StatsD address of its own container
+        self.metrics = None
         self._procs: Dict[str, _Proc] = {}
         self._lock = threading.Lock()
         self._native = None      # NativeLauncher once started; False: start processes in-process
@@ -510,7 +513,11 @@ class ProcessTaskBehavior(TaskBehavior):
             if src.type == P.Volume.Source.SECRET:
                 return None
             if src.type == P.Volume.Source.HOST_PATH or v.host_path:
-                link(src.host_path.path or v.host_path, v.container_path)
+                host_path = src.host_path.path or v.host_path
+                if not os.path.isabs(host_path):
+                    # a sandbox-relative host path (the SDK's `/tmp` -> `tmp` volume) exists
+                    steps.append(("d", os.path.join(sandbox, host_path)))
+                link(host_path, v.container_path)
             elif src.type == P.Volume.Source.SANDBOX_PATH:
                 target = os.path.join(sandbox, src.sandbox_path.path)
                 steps.append(("d", target))
@@ -585,7 +592,10 @@ class ProcessTaskBehavior(TaskBehavior):
                 with open(path, "wb") as f:
                     f.write(data or b"")
             elif src.type == P.Volume.Source.HOST_PATH or v.host_path:
-                self._link(src.host_path.path or v.host_path, sandbox, v.container_path)
+                host_path = src.host_path.path or v.host_path
+                if not os.path.isabs(host_path):
+                    os.makedirs(os.path.join(sandbox, host_path), exist_ok=True)
+                self._link(host_path, sandbox, v.container_path)
             elif src.type == P.Volume.Source.SANDBOX_PATH:
                 target = os.path.join(sandbox, src.sandbox_path.path)
                 os.makedirs(target, exist_ok=True)
@@ -660,6 +670,19 @@ class ProcessTaskBehavior(TaskBehavior):
             devs = ",".join(str(d) for d in task.gpu_devices)
             env["HIP_VISIBLE_DEVICES"] = devs
             env["ROCR_VISIBLE_DEVICES"] = devs
+        for v in task.info.container.volumes:
+            # the container's /tmp is the sandbox's `tmp` (PodInfoBuilder adds that volume to
+            # every task); without a mount namespace the task is pointed at it through TMPDIR
+            if v.container_path == "/tmp" and v.host_path and not os.path.isabs(v.host_path):
+                env["TMPDIR"] = os.path.join(sandbox, v.host_path)
+        if self.metrics is not None:
+            from dcos_commons_amd.mesos.local_master import container_id_for
+
+            env.update(self.metrics.container_env(
+                container_id_for(task.info.task_id.value), agent.id,
+                {"task_name": task.info.name, "task_id": task.info.task_id.value,
+                 "framework_id": task.framework_id, "executor_id": task.executor_id,
+                 "hostname": agent.spec.hostname}))
         return env
 
     # -- process supervision ----------------------------------------------------------

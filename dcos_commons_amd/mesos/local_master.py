@@ -213,6 +213,13 @@ class _Task:
     # the task's addresses as its statuses report them (``container_status.network_infos``)
     networks: List[P.NetworkInfo] = field(default_factory=list)
     reported_exit: bool = False   # its end came from its agent's runtime (no ``drop`` to send back)
+    container_id: str = ""        # what its statuses report as container_status.container_id
+
+
+def container_id_for(task_id: str) -> str:
+    """The container ID a task's statuses report (``container_status.container_id``; the local
+    cluster's metrics service files the task's StatsD under it): one per launch, as task IDs are."""
+    return str(uuid.uuid5(uuid.NAMESPACE_URL, "mesos-task:" + task_id))
 
 
 @dataclass
@@ -1206,6 +1213,9 @@ class LocalMaster:
             st.container_status.network_infos.extend(task.networks)
         else:
             st.container_status.network_infos.add().ip_addresses.add(ip_address="127.0.0.1")
+        if not task.container_id:
+            task.container_id = container_id_for(task.info.task_id.value)
+        st.container_status.container_id.value = task.container_id
         st.uuid = ids.uuid4_bytes()
         task.status = st
         if state in TERMINAL:

@@ -211,6 +211,7 @@ class LocalCluster:
             raise ValueError("gpu_probe_service needs executor='process' (the checks are task commands)")
         self.gpu_probe_service = gpu_probe_service
         self.probe_service = None
+        self.metrics = None   # testing.cluster.metrics.LocalMetrics, from start()
         self.http_master: Optional[HttpMaster] = None
         self.marathon = LocalMarathon(self)
         from dcos_commons_amd.testing.cluster.metronome import LocalMetronome
@@ -231,6 +232,11 @@ class LocalCluster:
 
                 self.probe_service = ProbeService(os.path.join(self.work_dir, "gpu-probe.sock")).start()
                 self.behavior.extra_env.update(self.probe_service.task_env)
+            from dcos_commons_amd.testing.cluster.metrics import LocalMetrics
+
+            self.metrics = LocalMetrics()
+            if hasattr(self.behavior, "metrics"):
+                self.behavior.metrics = self.metrics
             self.http_master = HttpMaster(self.master).start()
             for spec in self._agent_specs:
                 self.agent_ids[spec.hostname] = self.master.add_agent(spec)
@@ -250,6 +256,9 @@ class LocalCluster:
         self.master.shutdown()
         if self.probe_service is not None:
             self.probe_service.stop()
+        if self.metrics is not None:
+            self.metrics.stop()
+            self.metrics = None
         if self.zk is not None:
             self.zk.stop()
         if self.dcos is not None:

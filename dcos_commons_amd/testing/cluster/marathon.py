@@ -346,6 +346,14 @@ class LocalMarathon:
             "MESOS_TASK_ID": task.id, "MESOS_SANDBOX": task.sandbox, "HOST": task.host,
             "LIBPROCESS_IP": "127.0.0.1",
         })
+        if self.cluster.metrics is not None:
+            # a scheduler is a Marathon task: its StatsD reporter gets its container's socket
+            from dcos_commons_amd.mesos.local_master import container_id_for
+
+            env.update(self.cluster.metrics.container_env(
+                container_id_for(task.id), self.cluster.agent_ids.get(task.host, task.host),
+                {"task_name": app.id.strip("/"), "task_id": task.id, "framework_id": "marathon",
+                 "hostname": task.host}))
         pp = env.get("PYTHONPATH", os.environ.get("PYTHONPATH", ""))
         env["PYTHONPATH"] = REPO_ROOT + (os.pathsep + pp if pp else "")
         return env

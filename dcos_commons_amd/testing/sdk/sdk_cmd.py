@@ -166,6 +166,17 @@ def cluster_request(method: str, cluster_path: str, retry: bool = True, raise_on
                                "slave_id": t.agent_id} for t in c.tasks(include_terminal=True)]}
         elif path in ("/mesos_dns/v1/enumerate", "/mesos-dns/v1/enumerate"):
             body = c.dns_enumerate()
+        elif path.startswith("/system/v1/agent/") and "/metrics/v0/containers" in path and c.metrics is not None:
+            # dcos-metrics: /system/v1/agent/<agent>/metrics/v0/containers[/<container>/app]
+            agent_id, rest = path[len("/system/v1/agent/"):].split("/metrics/v0/containers", 1)
+            if not rest.strip("/"):
+                body = c.metrics.containers(agent_id)
+            elif rest.endswith("/app"):
+                body = c.metrics.app(rest.strip("/")[: -len("/app")].strip("/"))
+                if body is None:
+                    status, body = 404, {"message": f"no metrics for container {rest}"}
+            else:
+                status, body = 404, {"message": f"no such metrics endpoint: {path}"}
         elif path == "/dcos-metadata/dcos-version.json":
             body = {"version": c.dcos_version, "dcos-variant": "open"}
         elif path.startswith("/marathon/v2/groups"):
@@ -332,6 +343,19 @@ def run_cli(cmd: str, print_output: bool = True, check: bool = False) -> Tuple[i
         elif sub == "list":
             prefix = (path + "/") if path else ""
             rc, out, err = 0, "".join(f"- {k[len(prefix):]}\n" for k in sorted(c.secrets) if k.startswith(prefix)), ""
+    elif args[:3] == ["task", "metrics", "details"] and c.metrics is not None:
+        # dcos task metrics details [--json] <task id or name>: the task's container's datapoints
+        from dcos_commons_amd.mesos.local_master import container_id_for
+
+        target = [a for a in args[3:] if not a.startswith("--")][0]
+        ids = [target] if "." in target or "__" in target else []
+        if not ids:
+            ids = [t.id for t in c.tasks() if t.name == target]
+        app = c.metrics.app(container_id_for(ids[-1])) if ids else None
+        if app is None:
+            rc, out, err = 1, "", f"no metrics for task {target}\n"
+        else:
+            rc, out, err = 0, json.dumps(app["datapoints"]) + "\n", ""
     elif args[:2] == ["task", "exec"]:
         rc, out, err = service_task_exec(None, args[2], " ".join(args[3:]))
     elif args[:2] == ["task", "ls"]:

@@ -1,14 +1,17 @@
-"""Scheduler metrics (reference: testing/sdk_metrics.py, scheduler half).
+"""Scheduler and task metrics (reference: testing/sdk_metrics.py).
 
-The scheduler serves its Codahale-style registry at ``/v1/metrics`` (counters, gauges, timers);
-these helpers read and wait on it. Task metrics (dcos-metrics over StatsD) are not collected by the
-local cluster.
+The scheduler serves its Codahale-style registry at ``/v1/metrics`` (counters, gauges, timers), and
+pushes it over StatsD to its container's metrics socket. Task metrics go through dcos-metrics: a
+task writes StatsD to ``STATSD_UDP_HOST:STATSD_UDP_PORT`` and the agent's
+``/system/v1/agent/<agent>/metrics/v0/containers/<container>/app`` serves it (the local cluster's
+``testing.cluster.metrics``).
 """
 from __future__ import annotations
 
 import logging
 import time
-from typing import Any, Dict, Optional
+import json
+from typing import Any, Callable, Dict, List, Optional, Union
 
 from dcos_commons_amd.testing.sdk import sdk_cmd
 
@@ -58,8 +61,65 @@ def wait_for_scheduler_gauge_value(service_name: str, gauge_name: str, gauge_cal
 
 
 def check_metrics_presence(emitted_metrics, expected_metrics) -> bool:
-    names = set(emitted_metrics)
-    missing = [m for m in expected_metrics if m not in names]
+    """Whether every expected metric name was emitted (case-insensitive, as dcos-metrics may
+    normalize names)."""
+    names = {m.lower() for m in emitted_metrics}
+    missing = [m for m in expected_metrics if m.lower() not in names]
     if missing:
         LOG.info("Missing metrics: %s", missing)
     return not missing
+
+
+def get_metrics_from_cli(task_name: str) -> Union[Dict[str, Any], List[Dict[str, Any]]]:
+    """``dcos task metrics details --json <task>``: the datapoints of the task's container."""
+    rc, stdout, stderr = sdk_cmd.run_cli(f"task metrics details --json {task_name}")
+    if rc:
+        LOG.error("Error fetching metrics for %s: %s %s", task_name, stdout, stderr)
+        return {}
+    return list(json.loads(stdout))
+
+
+def wait_for_metrics_from_cli(task_name: str, timeout_seconds: int) -> List[Dict[str, Any]]:
+    deadline = time.time() + timeout_seconds
+    while True:
+        got = get_metrics_from_cli(task_name)
+        if got:
+            return list(got)
+        if time.time() >= deadline:
+            raise AssertionError(f"no metrics from task {task_name} within {timeout_seconds}s")
+        time.sleep(0.5)
+
+
+def get_metrics(package_name: str, service_name: str, pod_name: str, task_name: str) -> List[Dict[str, Any]]:
+    """The task's dcos-metrics datapoints: its container ID from its pod's latest status, checked
+    against the agent's container list, then the container's app metrics."""
+    from dcos_commons_amd.testing.sdk import sdk_tasks
+
+    task = next((t for t in sdk_tasks.get_service_tasks(service_name) if t.name == task_name), None)
+    if task is None:
+        raise Exception(f"Task named {task_name} not found in service {service_name}")
+    rc, stdout, _ = sdk_cmd.svc_cli(package_name, service_name, f"pod info {pod_name}", print_output=False)
+    assert rc == 0, "Pod info failed"
+    cid = next((p["status"]["containerStatus"]["containerId"]["value"] for p in json.loads(stdout)
+                if p["info"]["name"] == task_name and "status" in p), None)
+    if cid is None:
+        return []
+    listed = sdk_cmd.cluster_request("GET", f"/system/v1/agent/{task.agent_id}/metrics/v0/containers").json()
+    if cid not in listed:
+        raise ValueError(f"container {cid} of {task_name} not among the agent's metrics containers {listed}")
+    app = sdk_cmd.cluster_request("GET", f"/system/v1/agent/{task.agent_id}/metrics/v0/containers/{cid}/app").json()
+    if app.get("dimensions", {}).get("task_name") != task_name:
+        raise Exception(f"No metrics found for task {task_name} in service {service_name}")
+    return list(app["datapoints"])
+
+
+def wait_for_service_metrics(package_name: str, service_name: str, pod_name: str, task_name: str, timeout: int,
+                             expected_metrics_callback: Callable[[List[str]], bool]) -> List[str]:
+    deadline = time.time() + timeout
+    while True:
+        names = [m["name"] for m in get_metrics(package_name, service_name, pod_name, task_name)]
+        if expected_metrics_callback(names):
+            return names
+        if time.time() >= deadline:
+            raise AssertionError(f"metrics of {task_name} never matched: {names}")
+        time.sleep(0.5)

@@ -44,6 +44,44 @@ def test_scheduler_metrics():
     sdk_metrics.wait_for_scheduler_counter_value(FOLDERED, "task_status.task_running", 3)
 
 
+def test_metrics_cli_for_scheduler_metrics(configure_package):
+    """The scheduler (a Marathon task) pushes its registry over StatsD to its container's metrics
+    socket; ``dcos task metrics details`` shows it."""
+    prefix = sdk_marathon.get_scheduler_task_prefix(configure_package["service"]["name"])
+    task_id = sdk_tasks.get_task_ids("marathon", prefix).pop()
+    metrics = sdk_metrics.wait_for_metrics_from_cli(task_id, timeout_seconds=60)
+    assert metrics, "Expecting a non-empty set of metrics"
+    assert any(m["name"].startswith("offers.") for m in metrics), [m["name"] for m in metrics][:20]
+
+
+def test_metrics_for_task_metrics(configure_package):
+    """A task's StatsD datagram (to ``$STATSD_UDP_HOST:$STATSD_UDP_PORT``) appears in its
+    container's dcos-metrics datapoints."""
+    name = "test.metrics.CamelCaseMetric"
+    rc, _, err = sdk_cmd.service_task_exec(
+        FOLDERED, "hello-0-server", f"bash -c 'echo \"{name}:1|c\" > /dev/udp/$STATSD_UDP_HOST/$STATSD_UDP_PORT'")
+    assert rc == 0, err
+    sdk_metrics.wait_for_service_metrics(
+        configure_package["package_name"], FOLDERED, "hello-0", "hello-0-server", timeout=60,
+        expected_metrics_callback=lambda emitted: sdk_metrics.check_metrics_presence(emitted, [name]))
+
+
+def test_tmp_directory_created():
+    """Every task's /tmp is its sandbox's `tmp` directory (the volume PodInfoBuilder adds): it
+    exists, and what the task writes to its temporary directory lands there."""
+    rc, out, err = sdk_cmd.service_task_exec(
+        FOLDERED, "hello-0-server", "bash -c 'test -d tmp && echo bar > \"$TMPDIR/bar\" && cat tmp/bar'")
+    assert rc == 0 and out.strip() == "bar", (out, err)
+
+
+@needs_cli
+def test_help_cli():
+    rc, out, err = sdk_cmd.svc_cli(config.PACKAGE_NAME, FOLDERED, "help")
+    assert rc == 0, err
+    for sub in ("pod", "plan", "endpoints", "describe", "update"):
+        assert sub in out, out
+
+
 def test_bump_hello_cpus():
     hello_ids = sdk_tasks.get_task_ids(FOLDERED, "hello")
     world_ids = sdk_tasks.get_task_ids(FOLDERED, "world")
