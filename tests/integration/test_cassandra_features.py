@@ -1,7 +1,8 @@
 """Cassandra features on a strict-mode local cluster (synthetic task payloads).
 
 Reference: frameworks/cassandra/tests/{test_racks.py, test_overlay.py, test_custom_domain.py,
-test_toggle_tls.py, test_tls.py, test_backup_and_restore.py, test_auth.py}. Without Cassandra
+test_tls.py, test_backup_and_restore.py, test_auth.py, test_sanity.py}; test_toggle_tls.py is
+test_cassandra_toggle_tls.py. Without Cassandra
 binaries the checks stop at what the scheduler hands the nodes, rendered the way bootstrap renders
 it inside the task: ``cassandra-rackdc.properties`` names the node's zone as its rack when the
 placement references zones and the configured rack otherwise; the overlay network gives nodes
@@ -10,13 +11,14 @@ turning transport encryption on (with and without plaintext) and off again rolls
 mounting keystore artifacts from the secret store only while it is on; backup and restore plans
 run their phases in order; authentication settings reach ``cassandra.yaml``.
 """
+import json
 import urllib.parse
 
 import pytest
 
 from dcos_commons_amd.specification.yaml.template_utils import render_mustache
-from dcos_commons_amd.testing.sdk import (sdk_agents, sdk_cmd, sdk_install, sdk_networks, sdk_plan, sdk_security,
-                                          sdk_tasks, sdk_upgrade)
+from dcos_commons_amd.testing.sdk import (sdk_agents, sdk_cmd, sdk_install, sdk_networks, sdk_plan, sdk_recovery,
+                                          sdk_security, sdk_tasks, sdk_upgrade)
 from tests.integration.conftest import make_cluster
 from tests.integration.test_cassandra import ONCE_TASKS, PACKAGE
 
@@ -125,31 +127,42 @@ def _toggle(enabled, allow_plaintext):
     sdk_plan.wait_for_completed_deployment(SVC)
 
 
-def test_toggle_tls():
-    sdk_install.install(PACKAGE, SVC, 3, additional_options=ACCOUNT_OPTIONS)
+def test_custom_jmx_port():
+    """cassandra.jmx_port rolls every node onto the new JMX port (reference test_sanity.py
+    ``test_custom_jmx_port``; there ``lsof`` sees Cassandra listen on it)."""
+    sdk_install.install(PACKAGE, SVC, 3)
     try:
-        assert _keystore_volumes(0) == []
-        assert "internode_encryption: none" in _rendered(0, "cassandra")
-
-        _toggle(True, True)
+        ids = sdk_tasks.get_task_ids(SVC, "node")
+        sdk_upgrade.update_or_upgrade_or_downgrade(PACKAGE, SVC, to_version=None, expected_running_tasks=3,
+                                                   to_options={"cassandra": {"jmx_port": 7200}})
+        sdk_tasks.check_tasks_updated(SVC, "node", ids)
+        sdk_plan.wait_for_completed_deployment(SVC)
         for i in range(3):
-            vols = _keystore_volumes(i)
-            assert any(v.endswith("node.keystore") for v in vols) and any(v.endswith("node.truststore") for v in vols)
-        cfg = _rendered(0, "cassandra")
-        assert "internode_encryption: all" in cfg and "optional: true" in cfg
-        names = sdk_security.list_secrets(SVC)
-        assert any("keystore" in n for n in names) and any("truststore" in n for n in names)
-
-        _toggle(True, False)
-        cfg = _rendered(0, "cassandra")
-        assert "internode_encryption: all" in cfg and "optional: false" in cfg
-
-        _toggle(False, False)
-        assert _keystore_volumes(0) == []
-        assert "internode_encryption: none" in _rendered(0, "cassandra")
+            env = {v["name"]: v.get("value", "") for v in _server_info(i)["command"]["environment"]["variables"]}
+            assert env["JMX_PORT"] == "7200"
     finally:
         sdk_install.uninstall(PACKAGE, SVC)
-    assert not [n for n in sdk_security.list_secrets(SVC) if "keystore" in n or "truststore" in n]
+
+
+def test_tls_recovery():
+    """Every node of a TLS service replaced in turn: each replacement gets its TLS artifacts
+    mounted again and only the seed-list restarts touch other pods (reference test_tls.py
+    ``test_tls_recovery``)."""
+    sdk_install.install(PACKAGE, SVC, 3, additional_options=dict(
+        ACCOUNT_OPTIONS, service=dict(ACCOUNT_OPTIONS["service"],
+                                      security={"transport_encryption": {"enabled": True}})))
+    try:
+        rc, out, _ = sdk_cmd.svc_cli(PACKAGE, SVC, "pod list")
+        pods = json.loads(out)
+        for pod in pods:
+            i = int(pod.split("-")[1])
+            # replacing a seed (the first two nodes) restarts the others with the new seed list
+            sdk_recovery.check_permanent_recovery(PACKAGE, SVC, pod, recovery_timeout_s=300,
+                                                  pods_with_updated_tasks=pods if i < 2 else None)
+            vols = _keystore_volumes(i)
+            assert any(v.endswith("node.keystore") for v in vols) and any(v.endswith("node.truststore") for v in vols)
+    finally:
+        sdk_install.uninstall(PACKAGE, SVC)
 
 
 def test_backup_and_restore_plans():
