@@ -184,3 +184,18 @@ def test_permanently_replace_journalnodes():
     boots = [t for t in sdk_tasks.get_summary(with_completed=True) if t.name.startswith("journal-")
              and t.name.endswith("-bootstrap")]
     assert len(boots) >= 3 and all(t.state == "TASK_FINISHED" for t in boots)
+
+
+@needs_cli
+def test_namenodes_acheive_quorum_after_journalnode_replace():
+    """journal-0, journal-1, then journal-0 again replaced: every recovery completes and the name
+    nodes keep running (reference test_sanity.py; HDFS-10659 had the second replacement crash-loop
+    the name nodes)."""
+    names = sdk_tasks.get_task_ids(SVC, "name-")
+    for pod in ("journal-0", "journal-1", "journal-0"):
+        old = sdk_tasks.get_task_ids(SVC, f"{pod}-")
+        sdk_cmd.svc_cli(PACKAGE, SVC, f"pod replace {pod}", check=True)
+        sdk_tasks.check_tasks_updated(SVC, f"{pod}-", old)
+        sdk_plan.wait_for_completed_recovery(SVC)
+    sdk_tasks.check_tasks_not_updated(SVC, "name-", names)
+    check_healthy()

@@ -1,10 +1,9 @@
 """HDFS features on a strict-mode local cluster (synthetic task payloads).
 
-Reference: frameworks/hdfs/tests/{test_overlay.py, test_tls.py, test_racks.py, test_upgrade.py}.
+Reference: frameworks/hdfs/tests/{test_overlay.py, test_racks.py, test_upgrade.py}; test_tls.py is
+test_hdfs_tls.py.
 Every node type joins the overlay network (container addresses, no host ports) while the
-``hdfs-site.xml`` / ``core-site.xml`` endpoints keep being served; with transport encryption each
-journal, name and data node gets keystore artifacts from the cluster CA and ``hdfs-site.xml``
-switches to ``HTTPS_ONLY`` with the HTTPS addresses; zone placement makes data nodes rack-aware
+``hdfs-site.xml`` / ``core-site.xml`` endpoints keep being served; zone placement makes data nodes rack-aware
 (each sees its zone); the package upgrades to the newest published version and back.
 """
 import pytest
@@ -57,27 +56,6 @@ def test_tasks_and_endpoints_on_overlay():
         assert "dfs.namenode.rpc-address" in sdk_networks.get_endpoint_string(PACKAGE, SVC, "hdfs-site.xml")
     finally:
         sdk_install.uninstall(PACKAGE, SVC)
-
-
-def test_transport_encryption():
-    sdk_install.install(PACKAGE, SVC, DEFAULT_TASK_COUNT, additional_options=_opts({
-        "service": {"service_account": ACCOUNT, "service_account_secret": ACCOUNT_SECRET,
-                    "security": {"transport_encryption": {"enabled": True}}}}))
-    try:
-        site = sdk_networks.get_endpoint_string(PACKAGE, SVC, "hdfs-site.xml")
-        assert "HTTPS_ONLY" in site and "dfs.namenode.https-address" in site
-        for task in ("journal-0-node", "name-0-node", "name-1-node", "data-0-node"):
-            vols = [v["containerPath"] for v in _info(task).get("container", {}).get("volumes", [])
-                    if v.get("source", {}).get("type") == "SECRET"]
-            assert any(v.endswith(".keystore") for v in vols) and any(v.endswith(".truststore") for v in vols), \
-                (task, vols)
-        # one signed certificate per TLS-enabled task, stored under the service's secret namespace
-        names = sdk_security.list_secrets(SVC)
-        assert sum(1 for n in names if n.endswith("keystore")) >= 6, names
-        assert len(sdk_install._cluster().dcos.signed) >= 6
-    finally:
-        sdk_install.uninstall(PACKAGE, SVC)
-    assert not [n for n in sdk_security.list_secrets(SVC) if n.endswith(("keystore", "truststore"))]
 
 
 def test_detect_racks():
