@@ -33,7 +33,7 @@ def local_cluster():
 @pytest.fixture(scope="module", autouse=True)
 def tls_service(local_cluster):
     sdk_security.create_service_account(ACCOUNT, ACCOUNT_SECRET)
-    sdk_install.install(config.PACKAGE_NAME, config.SERVICE_NAME, 6, additional_options={
+    sdk_install.install(config.PACKAGE_NAME, config.SERVICE_NAME, 7, additional_options={
         "service": {"yaml": "tls", "service_account": ACCOUNT, "service_account_secret": ACCOUNT_SECRET},
         "hello": {"count": 2}, "tls": {"discovery_task_prefix": DISCOVERY_TASK_PREFIX}})
     sdk_plan.wait_for_completed_deployment(config.SERVICE_NAME)
@@ -105,6 +105,32 @@ def test_java_keystore_and_truststore():
     rc, _, _ = sdk_cmd.service_task_exec(config.SERVICE_NAME, "gateway-0-server", "ls gateway.crt")
     assert rc != 0
     assert _task_bytes("gateway-0-server", "gateway.keystore")
+
+
+def test_tls_nginx():
+    """The webserver task serves HTTPS with its mounted PEM certificate and key; a client in
+    another task, trusting only the cluster CA it was given, verifies the chain and the
+    certificate's name (the task's autoip host) and gets 200 (reference test_tls.py: NGINX and the
+    keystore app's ``truststoretest``)."""
+    info = next(t["info"] for t in sdk_cmd.service_request("GET", config.SERVICE_NAME,
+                                                             "/v1/pod/webserver-0/info").json())
+    port = next(p["number"] for p in info["discovery"]["ports"]["ports"] if p["name"] == "web-https")
+    host = sdk_hosts.autoip_host(config.SERVICE_NAME, "webserver-0-https")
+
+    @sdk_utils.retry(timeout_s=30, interval_s=0.5)
+    def fetch():
+        rc, out, err = sdk_cmd.service_task_exec(
+            config.SERVICE_NAME, "artifacts-0-node",
+            f"python3 -m dcos_commons_amd.testing.tls_probe get --ca artifacts.ca --host {host} "
+            f"--connect 127.0.0.1:{port}")
+        assert rc == 0 and "status=200" in out, (out, err)
+    fetch()
+    # a name the certificate does not carry is refused
+    rc, out, err = sdk_cmd.service_task_exec(
+        config.SERVICE_NAME, "artifacts-0-node",
+        f"python3 -m dcos_commons_amd.testing.tls_probe get --ca artifacts.ca --host not-the-task.example "
+        f"--connect 127.0.0.1:{port}")
+    assert rc != 0 and "status=200" not in out
 
 
 def test_tls_secrets_in_store():
