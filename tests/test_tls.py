@@ -228,11 +228,11 @@ def test_tls_service_deploys_with_secret_volumes_and_uninstall_cleans_up(dcos):
                  DCOS_SPACE="/folder/tls-svc") as c:
         c.wait_plan("deploy", timeout=60)
         states = c.master.task_states()
-        assert len(states) == 7 and set(states.values()) == {P.TASK_RUNNING}
+        assert len(states) == 8 and set(states.values()) == {P.TASK_RUNNING}
         # 5 artifacts per transport-encryption entry per task instance:
-        # artifacts 2x2, gateway 2x1, discovery 1, multi 2 -> 9 entries
+        # artifacts 2x2, gateway 2x1, discovery 1, webserver 1, multi 2 -> 10 entries
         ns = "folder/tls-svc"
-        assert len([k for k in dcos.secrets if k.startswith(ns + "/")]) == 45
+        assert len([k for k in dcos.secrets if k.startswith(ns + "/")]) == 50
         tasks = {t.name: t for t in c.master.tasks_by_name().values()}
         vols = {v.container_path: v for v in tasks["artifacts-0-node"].container.volumes}
         assert {"artifacts.crt", "artifacts.key", "artifacts.ca", "store.keystore", "store.truststore"} <= set(vols)
