@@ -91,3 +91,19 @@ def test_framework_scheduler_wires_the_gate_only_when_enabled():
     # a driver without the hook (the in-process LocalMaster's) is left alone
     FrameworkScheduler([], SchedulerConfig.for_testing(), None, None, None,
                        offer_processor=_processor())._gate_statuses(object())
+
+
+def test_no_gate_with_a_remote_persister():
+    """With ZooKeeper state the cycle and the statuses both wait on round trips: no gate."""
+    class Remote:
+        remote = True
+
+    class Drv:
+        gate = None
+
+        def set_status_gate(self, g):
+            self.gate = g
+    fs = FrameworkScheduler([], SchedulerConfig.for_testing(), Remote(), None, None, offer_processor=_processor())
+    drv = Drv()
+    fs._gate_statuses(drv)
+    assert drv.gate is None
