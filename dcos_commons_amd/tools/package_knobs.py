@@ -53,10 +53,6 @@ _C = [
     ("hints_flush_period_in_ms", "integer", 10000, "How often hints are flushed to disk"),
     ("max_hints_file_size_in_mb", "integer", 128, "Maximum size of one hints file"),
     ("batchlog_replay_throttle_in_kb", "integer", 1024, "Batchlog replay throttle"),
-    ("role_manager", "string", "CassandraRoleManager", "Role manager implementation"),
-    ("roles_validity_in_ms", "integer", 2000, "Validity of the roles cache"),
-    ("permissions_validity_in_ms", "integer", 2000, "Validity of the permissions cache"),
-    ("credentials_validity_in_ms", "integer", 2000, "Validity of the credentials cache"),
     ("disk_failure_policy", "string", "stop", "Policy on a data disk failure: die, stop_paranoid, stop, best_effort, ignore"),
     ("commit_failure_policy", "string", "stop", "Policy on a commit log failure: die, stop, stop_commit, ignore"),
     ("prepared_statements_cache_size_mb", "string", "", "Prepared statements cache size (empty: auto)"),
@@ -138,6 +134,21 @@ _C = [
     ("buffer_pool_use_heap_if_exhausted", "boolean", True, "Allocate on heap when the buffer pool is exhausted"),
     ("file_cache_size_in_mb", "string", "", "SSTable chunk cache (empty: min(512 MB, 1/4 of heap))"),
     ("cdc_enabled", "boolean", False, "Change data capture"),
+    ("cdc_total_space_in_mb", "integer", 4096, "Space for CDC logs before writes to CDC tables fail"),
+    ("cdc_free_space_check_interval_ms", "integer", 250, "CDC space recheck interval once the cap is hit"),
+    ("start_native_transport", "boolean", True, "Serve the native (CQL) protocol"),
+    ("commitlog_sync_batch_window_in_ms", "string", "", "Batch commit log window (batch sync only; empty: unset)"),
+    ("key_cache_keys_to_save", "integer", 100, "Key cache keys saved (0: all)"),
+    ("row_cache_keys_to_save", "integer", 100, "Row cache keys saved (0: all)"),
+    ("counter_cache_keys_to_save", "integer", 100, "Counter cache keys saved (0: all)"),
+    ("memtable_cleanup_threshold", "number", 0.11, "Memtable fill ratio that triggers a flush of the largest"),
+    ("internode_authenticator", "string", "org.apache.cassandra.auth.AllowAllInternodeAuthenticator",
+     "Authenticator of internode connections"),
+    ("rpc_min_threads", "integer", 16, "Thrift request threads (minimum)"),
+    ("rpc_max_threads", "integer", 2048, "Thrift request threads (maximum)"),
+    ("rpc_send_buff_size_in_bytes", "integer", 16384, "Thrift socket send buffer"),
+    ("rpc_recv_buff_size_in_bytes", "integer", 16384, "Thrift socket receive buffer"),
+    ("windows_timer_interval", "integer", 1, "Windows timer resolution (ms; ignored elsewhere)"),
     ("repair_session_max_tree_depth", "integer", 18, "Merkle tree depth of a repair session"),
     ("listen_on_broadcast_address", "boolean", False, "Also listen on the broadcast address"),
     ("auto_bootstrap", "boolean", True, "Stream data to a new node when it joins"),

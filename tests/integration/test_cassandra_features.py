@@ -191,11 +191,32 @@ def test_backup_and_restore_plans():
 
 
 def test_authentication_settings():
-    sdk_install.install(PACKAGE, SVC, 3, additional_options={
-        "service": {"security": {"authentication": {"enabled": True, "superuser": {"name": "admin"}}}}})
+    """PasswordAuthenticator with the superuser's password from the secret store and
+    CassandraAuthorizer, then authorization switched off by an update that rolls every node
+    (reference cassandra config.json ``service.security.authentication/authorization``)."""
+    c = sdk_install._cluster()
+    c.secrets[f"{SVC.strip('/')}/superuser-pw"] = b"s3cret"
+    sdk_install.install(PACKAGE, SVC, 3, additional_options={"service": {"security": {
+        "authentication": {"enabled": True, "superuser": {"name": "admin",
+                                                           "password_secret_path": f"{SVC.strip('/')}/superuser-pw"}},
+        "authorization": {"enabled": True, "roles_validity_in_ms": 5000}}}})
     try:
+        for i in range(3):
+            cfg = _rendered(i, "cassandra")
+            assert "authenticator: PasswordAuthenticator" in cfg and "authorizer: CassandraAuthorizer" in cfg
+            assert "roles_validity_in_ms: 5000" in cfg
+            assert _keystore_volumes(i) == ["superuser/password"]
+        init = next(t["info"] for t in sdk_cmd.service_request("GET", SVC, "/v1/pod/node-0/info").json()
+                    if t["info"]["name"] == "node-0-init_system_keyspaces")
+        assert "CREATE ROLE" in init["command"]["value"]
+        ids = sdk_tasks.get_task_ids(SVC, "node")
+        sdk_upgrade.update_or_upgrade_or_downgrade(
+            PACKAGE, SVC, to_version=None, expected_running_tasks=3,
+            to_options={"service": {"security": {"authorization": {"enabled": False}}}})
+        sdk_tasks.check_tasks_updated(SVC, "node", ids)
+        sdk_plan.wait_for_completed_deployment(SVC)
         cfg = _rendered(0, "cassandra")
-        assert "authenticator: PasswordAuthenticator" in cfg
+        assert "authenticator: PasswordAuthenticator" in cfg and "authorizer: AllowAllAuthorizer" in cfg
     finally:
         sdk_install.uninstall(PACKAGE, SVC)
 

@@ -60,6 +60,96 @@ def test_cassandra_tls_cqlsh_and_metrics_off():
     assert "metricsReporterConfigFile" not in r.service_spec.pod("node").task("server").command.value
 
 
+def test_cassandra_access_control_defaults():
+    """Without service.security.authentication/authorization the nodes run AllowAll*; the cache and
+    back-pressure settings carry the package defaults (reference cassandra config.json)."""
+    import yaml
+    cfg = yaml.safe_load(test_cassandra.runner().run().get_task_config("node", "server", "cassandra"))
+    assert cfg["authenticator"] == "AllowAllAuthenticator" and cfg["authorizer"] == "AllowAllAuthorizer"
+    assert cfg["role_manager"] == "CassandraRoleManager" and cfg["permissions_cache_max_entries"] == 1000
+    for name in ("roles", "credentials", "permissions"):
+        assert cfg[f"{name}_validity_in_ms"] == 2000 and cfg[f"{name}_update_interval_in_ms"] == 2000
+    assert cfg["seed_provider"][0]["class_name"] == "org.apache.cassandra.locator.SimpleSeedProvider"
+    (bp,) = cfg["back_pressure_strategy"]
+    assert bp["class_name"].endswith("RateBasedBackPressure")
+    assert bp["parameters"] == [{"high_ratio": 0.9, "factor": 5, "flow": "FAST"}]
+    assert cfg["start_native_transport"] is True and "commitlog_sync_batch_window_in_ms" not in cfg
+
+
+def test_cassandra_authentication_and_authorization(tmp_path):
+    """PasswordAuthenticator + CassandraAuthorizer with a superuser password secret: the secret is
+    mounted in the node pod (merged with the secure JMX secrets when both are on), and the init
+    step replaces the default login by the configured superuser before altering system_auth."""
+    import base64
+    import yaml
+    custom = base64.b64encode(b"auth_read_consistency_level: LOCAL_QUORUM").decode()
+    r = (test_cassandra.runner().set_options(
+        "service.security.authentication.enabled", "true",
+        "service.security.authentication.superuser.name", "admin",
+        "service.security.authentication.superuser.password_secret_path", "cassandra/su-pw",
+        "service.security.authentication.authentication_custom_cassandra_yml", custom,
+        "service.security.authorization.enabled", "true",
+        "service.security.authorization.permissions_validity_in_ms", "0",
+        "service.jmx.enabled", "true", "service.jmx.password_file", "c/jmx-pw", "service.jmx.access_file", "c/acc",
+        "service.jmx.key_store", "c/ks", "service.jmx.key_store_password_file", "c/ks-pw",
+        "service.rlimits.rlimit_nofile.soft", "200000", "service.rlimits.rlimit_nofile.hard", "300000",
+        "cassandra.back_pressure_flow", "SLOW").run())
+    cfg = yaml.safe_load(r.get_task_config("node", "server", "cassandra"))
+    assert cfg["authenticator"] == "PasswordAuthenticator" and cfg["authorizer"] == "CassandraAuthorizer"
+    assert cfg["permissions_validity_in_ms"] == 0
+    assert cfg["back_pressure_strategy"][0]["parameters"][0]["flow"] == "SLOW"
+    pod = r.service_spec.pod("node")
+    files = sorted(s.file_path for s in pod.secrets)
+    assert files == ["jmx/access_file", "jmx/key_store", "jmx/key_store_password_file", "jmx/password_file",
+                     "superuser/password"]
+    assert next(s for s in pod.secrets if s.file_path == "superuser/password").secret_path == "cassandra/su-pw"
+    (rl,) = pod.rlimits
+    assert (rl.soft, rl.hard) == (200000, 300000)
+    # the init step's script, with a stub cqlsh that logs its arguments
+    init = pod.task("init_system_keyspaces").command.value
+    sandbox = tmp_path / "sb"
+    (sandbox / "apache-cassandra-3.11.6" / "bin").mkdir(parents=True)
+    (sandbox / "superuser").mkdir()
+    (sandbox / "superuser" / "password").write_text("s3cret")
+    log = sandbox / "cqlsh.log"
+    stub = sandbox / "apache-cassandra-3.11.6" / "bin" / "cqlsh"
+    stub.write_text(f'#!/bin/bash\necho "$*" >> {log}\ncase "$*" in *"CREATE ROLE"*) touch {sandbox}/created;; esac\n'
+                    f'[ "$2" != admin ] || [ -f {sandbox}/created ]\n')     # admin logs in once created
+    stub.chmod(0o755)
+    script = init.replace("{{CASSANDRA_VERSION}}", "3.11.6")
+    env = dict(os.environ, CASSANDRA_AUTHENTICATOR="PasswordAuthenticator", SUPERUSER_NAME="admin",
+               FRAMEWORK_HOST="cassandra.autoip", CASSANDRA_NATIVE_TRANSPORT_PORT="9042",
+               CASSANDRA_LOCATION_DATA_CENTER="dc1")
+    for _ in range(2):     # a rerun finds the superuser and does not recreate it
+        subprocess.run(["bash", "-c", script], cwd=sandbox, env=env, check=True)
+    lines = log.read_text().splitlines()
+    creates = [l for l in lines if "CREATE ROLE" in l]
+    assert len(creates) == 1 and creates[0].startswith("-u cassandra -p cassandra") and "'s3cret'" in creates[0]
+    assert any("ALTER ROLE cassandra" in l and "SUPERUSER = false" in l for l in lines)
+    alters = [l for l in lines if "ALTER KEYSPACE system_auth" in l]
+    assert len(alters) == 2 and all(l.startswith("-u admin -p s3cret") for l in alters)
+
+
+def test_cassandra_marathon_health_check_rlimits_and_profile():
+    app = render_marathon_app(os.path.join(ROOT, "frameworks", "cassandra", "universe"), {})
+    (hc,) = app["healthChecks"]
+    assert (hc["intervalSeconds"], hc["timeoutSeconds"], hc["delaySeconds"]) == (30, 20, 15)
+    env = app["env"]
+    assert env["RLIMIT_NOFILE_SOFT"] == env["RLIMIT_NOFILE_HARD"] == "128000"
+    assert "CASSANDRA_VOLUME_PROFILE" not in env and "NODE_POD_SECRETS" not in env
+    assert env["TASKCFG_ALL_CASSANDRA_AUTHENTICATOR"] == "AllowAllAuthenticator"
+    app = render_marathon_app(os.path.join(ROOT, "frameworks", "cassandra", "universe"),
+                              {"nodes.volume_profile": "xfs", "service.security.authentication.enabled": "true",
+                               "service.security.authentication.superuser.password_secret_path": "c/pw",
+                               "service.security.authentication.authentication_custom_cassandra_yml": "YTogYg=="})
+    env = app["env"]
+    assert env["CASSANDRA_VOLUME_PROFILE"] == "xfs" and env["NODE_POD_SECRETS"] == "yes"
+    assert env["TASKCFG_ALL_CASSANDRA_AUTHENTICATOR"] == "PasswordAuthenticator"
+    assert env["SUPERUSER_PASSWORD_SECRET"] == "c/pw"
+    # decoded by the scheduler into every node's cassandra.yaml (models/cassandra.py)
+    assert env["TASKCFG_ALL_AUTHENTICATION_CUSTOM_YAML_BLOCK_BASE64"] == "YTogYg=="
+
+
 def test_cassandra_secure_jmx(tmp_path):
     r = (test_cassandra.runner()
          .set_options("service.jmx.enabled", "true", "service.jmx.password_file", "cassandra/jmx-pw",
