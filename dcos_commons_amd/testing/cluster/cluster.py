@@ -131,10 +131,11 @@ class TaskView:
 class _SyntheticBehavior(TaskBehavior):
     """Synthetic lifecycle; tasks whose name ends with one of ``finish_suffixes`` exit 0."""
 
-    def __init__(self, finish_suffixes: Sequence[str], finish_after_s: float = 0.2):
-        super().__init__(TaskTiming())
+    def __init__(self, finish_suffixes: Sequence[str], finish_after_s: float = 0.2, honor_check_delays: bool = True):
+        super().__init__(TaskTiming(honor_check_delays=honor_check_delays))
         self.finish_suffixes = tuple(finish_suffixes)
-        self.finish = TaskTiming(finish_after_s=finish_after_s, exit_state=P.TASK_FINISHED)
+        self.finish = TaskTiming(finish_after_s=finish_after_s, exit_state=P.TASK_FINISHED,
+                                 honor_check_delays=honor_check_delays)
 
     def timing(self, task: P.TaskInfo) -> TaskTiming:
         if self.finish_suffixes and task.name.endswith(self.finish_suffixes):
@@ -150,7 +151,8 @@ class LocalCluster:
                  packages: Optional[Dict[str, str]] = None, scheduler_env: Optional[Dict[str, str]] = None,
                  finish_tasks: Sequence[str] = (), dcos_version: str = "1.13.0", keep_work_dir: bool = False,
                  mount_disks: Sequence[tuple] = (), dcos_security: bool = False, zk_process: bool = False,
-                 gpu_probe_service: bool = False, gpu_inventory=None, finish_after_s: float = 0.2):
+                 gpu_probe_service: bool = False, gpu_inventory=None, finish_after_s: float = 0.2,
+                 honor_check_delays: bool = True):
         self.work_dir = os.path.abspath(work_dir or tempfile.mkdtemp(prefix="sdk-cluster-"))
         self._own_work_dir = work_dir is None and not keep_work_dir
         self.region = region
@@ -181,8 +183,10 @@ class LocalCluster:
                                                 secret_resolver=self.resolve_secret, resolver=self.resolve,
                                                 artifact_resolver=self.resolve_artifact, extra_env=task_env)
         elif executor == "synthetic":
-            # finish_after_s: how long a synthetic ONCE/FINISH task runs before it exits 0
-            self.behavior = _SyntheticBehavior(finish_tasks, finish_after_s)
+            # finish_after_s: how long a synthetic ONCE/FINISH task runs before it exits 0;
+            # honor_check_delays=False starts readiness checks at once (a package's check delay
+            # covers a real process's start-up, which a synthetic task does not have)
+            self.behavior = _SyntheticBehavior(finish_tasks, finish_after_s, honor_check_delays)
         else:
             raise ValueError(f"executor must be 'process' or 'synthetic', not {executor!r}")
         self.executor = executor

@@ -19,12 +19,12 @@ PACKAGE = "hdfs"
 SVC = "/test/integration/hdfs"
 DEFAULT_TASK_COUNT = 10           # 3 journal + 2 name + 2 zkfc + 3 data
 FINISH_TASKS = ("-format", "-bootstrap", "-zkfc-format")
-APP_CONFIG_FIELD = "TASKCFG_ALL_HDFS_NAME_NODE_HANDLER_COUNT"
+APP_CONFIG_FIELD = "TASKCFG_ALL_CLIENT_READ_SHORTCIRCUIT_STREAMS_CACHE_EXPIRY_MS"   # the reference test_sanity.py field
 
 
 @pytest.fixture(scope="module", autouse=True)
 def hdfs_cluster():
-    c = make_cluster(executor="synthetic", finish_tasks=FINISH_TASKS)
+    c = make_cluster(executor="synthetic", finish_tasks=FINISH_TASKS, honor_check_delays=False)
     # (data nodes pass their first readiness check after 1 s instead of the default 10 s)
     sdk_install.install(PACKAGE, SVC, DEFAULT_TASK_COUNT,
                         additional_options={"data_node": {"readiness_check": {"delay": 1, "interval": 1}}})

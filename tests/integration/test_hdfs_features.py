@@ -27,7 +27,7 @@ def _opts(extra):
 
 @pytest.fixture(scope="module")
 def local_cluster():
-    c = make_cluster(executor="synthetic", finish_tasks=FINISH_TASKS, dcos_security=True)
+    c = make_cluster(executor="synthetic", finish_tasks=FINISH_TASKS, dcos_security=True, honor_check_delays=False)
     sdk_security.create_service_account(ACCOUNT, ACCOUNT_SECRET)
     yield c
     c.shutdown()
@@ -60,7 +60,7 @@ def test_tasks_and_endpoints_on_overlay():
 
 def test_detect_racks():
     sdk_install.install(PACKAGE, SVC, DEFAULT_TASK_COUNT, additional_options=_opts({
-        "data_node": {"placement_constraint": '[["@zone", "GROUP_BY", "3"]]'}}))
+        "data_node": {"placement": '[["@zone", "GROUP_BY", "3"]]'}}))
     try:
         zones = {a["hostname"]: a["zone"] for a in sdk_agents.get_agents()}
         data = [t for t in sdk_tasks.get_service_tasks(SVC) if t.name.startswith("data-")]

@@ -41,7 +41,7 @@ def test_spec_renders_every_config():
     assert "name-1-node.hdfs.autoip.dcos.thisdcos.directory:9001" in hdfs_site
     assert "https-address" not in hdfs_site
     core = r.get_task_config("data", "node", "core-site")
-    assert "/dcos-service-hdfs/hadoop-ha" in core and "kerberos" not in core
+    assert "/dcos-service-hdfs/hadoop-ha" in core and "<value>kerberos</value>" not in core
     assert sorted(r.raw_service_spec.plans) == ["deploy", "replace", "update"]
 
 
@@ -82,7 +82,7 @@ def _zone_spec(placement):
     r = ServiceTestRunner.for_framework("hdfs")
     for pod in ("journal", "name", "data"):
         r.set_pod_env(pod, SERVICE_ZK_ROOT="", DECODED_AUTH_TO_LOCAL="")
-    return r.set_options("data_node.placement_constraint", placement).run().service_spec
+    return r.set_options("data_node.placement", placement).run().service_spec
 
 
 def test_zone_validator():

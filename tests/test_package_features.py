@@ -220,6 +220,108 @@ def test_hdfs_https_with_tls():
     assert "ssl-client" in names and "ssl-server" not in names
 
 
+def test_hdfs_node_type_options():
+    """Per node type: rlimits, volume profile, placement, readiness checks (reference hdfs
+    config.json journal_node / name_node / data_node sections)."""
+    r = _hdfs(**{"journal_node.rlimits.rlimit_nofile.soft": "200000", "journal_node.rlimits.rlimit_nofile.hard": "200000",
+                 "name_node.rlimits.rlimit_nofile.hard": "300000",
+                 "data_node.volume_profile": "xfs", "data_node.disk_type": "MOUNT",
+                 "name_node.placement": '[["hostname", "UNIQUE"]]',
+                 "journal_node.readiness_check.interval": "7", "journal_node.lagging_tx_count": "5",
+                 "name_node.readiness_check.timeout": "99"})
+    spec = r.service_spec
+    assert spec.pod("journal").rlimits[0].soft == 200000 and spec.pod("name").rlimits[0].hard == 300000
+    assert spec.pod("data").rlimits[0].soft == 128000
+    assert "xfs" in repr(spec.pod("data").task("node").resource_set)
+    assert "MaxPerHostname" in repr(spec.pod("name").placement_rule)     # hostname:UNIQUE
+    jrc = spec.pod("journal").task("node").readiness_check
+    assert jrc.interval == 7 and "CurrentLagTxns" in jrc.command and "-le 5" in jrc.command
+    assert spec.pod("name").task("node").readiness_check.timeout == 99
+    r = _hdfs(**{"journal_node.enable_readiness_check": "false"})
+    assert r.service_spec.pod("journal").task("node").readiness_check is None
+
+
+def test_hdfs_journal_readiness_check_script(tmp_path):
+    """The JournalNode readiness check passes on a first deployment (no journal yet) and then only
+    while the journal's CurrentLagTxns metric is within journal_node.lagging_tx_count."""
+    cmd = _hdfs(**{"journal_node.lagging_tx_count": "5"}).service_spec.pod("journal").task("node").readiness_check.command
+    (tmp_path / "bin").mkdir()
+    curl = tmp_path / "bin" / "curl"
+    env = dict(os.environ, PATH=f"{tmp_path / 'bin'}:{os.environ['PATH']}", MESOS_CONTAINER_IP="127.0.0.1")
+
+    def check(lag):
+        curl.write_text('#!/bin/bash\necho \'{"beans" : [ {"name" : "Hadoop:service=JournalNode,name=Journal-hdfs",'
+                        f'\n "CurrentLagTxns" : {lag}, "LastWrittenTxId" : 42 }} ] }}\'\n')
+        curl.chmod(0o755)
+        return subprocess.run(["bash", "-c", cmd], cwd=tmp_path, env=env).returncode == 0
+
+    assert check(100)                              # no journal-data/hdfs: first deployment
+    (tmp_path / "journal-data" / "hdfs").mkdir(parents=True)
+    assert check(3) and check(5) and not check(6)
+
+
+def test_hdfs_security_and_plaintext_options():
+    r = _hdfs(**{"service.security.transport_encryption.enabled": "true",
+                 "service.security.transport_encryption.allow_plaintext": "true",
+                 "hdfs.block_access_token_enable": "true", "hdfs.security_authorization": "false",
+                 "name_node.handler_count": "40", "hdfs.ha_fencing_methods": "shell(/bin/false)"})
+    site = _props(r.get_task_config("name", "node", "hdfs-site"))
+    assert site["dfs.http.policy"] == "HTTP_AND_HTTPS" and site["dfs.block.access.token.enable"] == "true"
+    assert site["dfs.namenode.handler.count"] == "40" and site["dfs.ha.fencing.methods"] == "shell(/bin/false)"
+    assert _props(r.get_task_config("name", "node", "core-site"))["hadoop.security.authorization"] == "false"
+    # defaults: plaintext HTTP off, authorization on, tokens off
+    r = _hdfs()
+    site = _props(r.get_task_config("data", "node", "hdfs-site"))
+    assert site["dfs.block.access.token.enable"] == "false" and site["dfs.namenode.handler.count"] == "10"
+    assert _props(r.get_task_config("data", "node", "core-site"))["hadoop.security.authorization"] == "true"
+
+
+def test_hdfs_site_files_have_no_duplicate_properties():
+    for opts in ({}, {"service.security.transport_encryption.enabled": "true"}):
+        r = _hdfs(**opts)
+        for pod in ("journal", "name", "data"):
+            for name in ("hdfs-site", "core-site"):
+                names = [p.findtext("name") for p in ET.fromstring(r.get_task_config(pod, "node", name)).iter("property")]
+                assert len(names) == len(set(names)), (pod, name, {n for n in names if names.count(n) > 1})
+
+
+def test_hdfs_marathon_env_and_health_check():
+    app = render_marathon_app(os.path.join(ROOT, "frameworks", "hdfs", "universe"),
+                              {"name_node.hadoop_namenode_opts": "-XX:+UseG1GC", "hdfs.hadoop_heapsize": "2048",
+                               "service.security.custom_domain": "example.tld"})
+    (hc,) = app["healthChecks"]
+    assert (hc["intervalSeconds"], hc["timeoutSeconds"], hc["delaySeconds"]) == (30, 20, 15)
+    env = app["env"]
+    assert env["TASKCFG_ALL_HADOOP_NAMENODE_OPTS"] == "-XX:+UseG1GC" and env["TASKCFG_ALL_HADOOP_HEAPSIZE"] == "2048"
+    assert env["TASKCFG_ALL_HADOOP_ROOT_LOGGER"] == "INFO,console" and env["SERVICE_TLD"] == "example.tld"
+    assert env["JOURNAL_READINESS_CHECK_ENABLED"] == "true" and env["NAME_NODE_READINESS_CHECK_TIMEOUT"] == "180"
+    # reference option paths of renamed knobs, with the reference package's defaults
+    assert env["TASKCFG_ALL_NAME_NODE_HEARTBEAT_RECHECK_INTERVAL"] == "60000"
+    assert env["TASKCFG_ALL_CLIENT_READ_SHORTCIRCUIT_STREAMS_CACHE_EXPIRY_MS"]
+
+
+@pytest.mark.skipif(not os.path.isdir("/root/reference/frameworks"), reason="no reference tree")
+@pytest.mark.parametrize("framework", ["helloworld", "cassandra", "hdfs"])
+def test_every_reference_option_path_exists(framework):
+    """An options file written for the reference package installs unchanged: every leaf option of
+    its universe/config.json is a leaf of ours (the debug.* JVM-debugger options of the reference
+    helloworld scheduler have no counterpart: the scheduler is not a JVM)."""
+    import json
+
+    def leaves(d, p=""):
+        out = {}
+        for k, v in d.get("properties", {}).items():
+            out.update(leaves(v, p + k + ".") if v.get("type") == "object" and "properties" in v else {p + k: v})
+        return out
+
+    with open(f"/root/reference/frameworks/{framework}/universe/config.json", encoding="utf-8") as f:
+        ref = leaves(json.load(f))
+    with open(os.path.join(ROOT, "frameworks", framework, "universe", "config.json"), encoding="utf-8") as f:
+        ours = leaves(json.load(f))
+    missing = sorted(k for k in ref if k not in ours and not k.startswith("debug."))
+    assert not missing, missing
+
+
 def test_hdfs_kerberos_krb5_conf_and_jvm_flag():
     r = _hdfs(**{"service.security.kerberos.enabled": "true", "service.security.kerberos.realm": "EXAMPLE.COM",
                  "service.security.kerberos.kdc.hostname": "kdc.example.com",
