@@ -22,6 +22,7 @@ ap.add_argument("n", type=int)
 ap.add_argument("--cycles", type=int, default=30)
 ap.add_argument("--sort", default="tottime")
 ap.add_argument("--limit", type=int, default=45)
+ap.add_argument("--callers", default="", help="also print the callers of functions matching this pattern")
 args = ap.parse_args()
 
 proc, ports = MP.spawn()
@@ -70,6 +71,8 @@ st = pstats.Stats(profiles[0])
 for p in profiles[1:]:
     st.add(p)
 st.sort_stats(args.sort).print_stats(args.limit)
+if args.callers:
+    st.print_callers(args.callers)
 client.call("shutdown")
 proc.wait(10)
 for k in kids:
