@@ -121,8 +121,13 @@ class FrameworkRunner:
         info = self.get_framework_info(framework_store.fetch_framework_id())
         factory = self.driver_factory or self._default_driver_factory()
         self.driver = factory(self.framework_scheduler, info)
+        prestart = self.scheduler_config.thread_prestart()
+        if prestart == "before" or (prestart == "after" and block):
+            self.framework_scheduler.prestart()
         if not block:
             self.driver.start()
+            if prestart == "after":
+                self.framework_scheduler.prestart()
             return self.driver
         self.driver.run()
         self.api_server.join()

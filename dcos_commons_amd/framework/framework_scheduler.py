@@ -118,6 +118,13 @@ class FrameworkScheduler:
             set_gate(lambda: processor.wait_cycle_idle(wait_s))
 
     # -- Mesos callbacks ---------------------------------------------------------------
+    def prestart(self) -> None:
+        """Create the offer-loop and reconciler threads before the driver subscribes (both wait
+        for registration), so that the ``registered`` callback does not pay for thread start-up
+        while the first offers queue behind it."""
+        self.offer_processor.prestart()
+        self.implicit_reconciler.prestart()
+
     def registered(self, driver, framework_id: P.FrameworkID, master_info) -> None:
         trace.instant("registered", "driver")
         try:

@@ -310,6 +310,16 @@ class SchedulerConfig:
         2.02 -> 2.27 ms (profiles/prewarm_window_ab_r06_box.txt)."""
         return self.env.get_optional_boolean("SDK_OFFER_PREWARM", False)
 
+    def thread_prestart(self) -> str:
+        """When the offer-loop and implicit-reconciler threads are created (``SDK_THREAD_PRESTART``;
+        ``FrameworkScheduler.prestart``): ``before`` SUBSCRIBE goes out, ``after`` it (a
+        non-blocking driver: thread start-up overlaps the registration round trip), or ``false``
+        (default): in the ``registered`` callback, as the reference starts its offer loop. Not
+        adopted: on the box all three were within the spread, 1 pod 1.94-1.97 ms and 8 pods
+        5.26-5.29 ms best of three (profiles/prestart_ab_r06_box.txt)."""
+        v = self.env.get_optional("SDK_THREAD_PRESTART", "false").strip().lower()
+        return {"true": "before", "1": "before", "0": "false", "no": "false"}.get(v, v)
+
     def offer_hold_s(self) -> float:
         """Hold unused offers this long while WORKING instead of declining them for 1 h
         (0 = reference behaviour: long decline + rate-limited revive)."""

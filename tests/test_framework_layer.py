@@ -339,6 +339,45 @@ def test_implicit_reconciler(drv):
     assert len(drv.reconciles) >= 3
 
 
+def test_implicit_reconciler_prestart_waits_for_start(drv):
+    """A thread created ahead of registration reconciles nothing until ``start``; ``stop`` ends a
+    thread that was never started."""
+    r = ImplicitReconciler(0.0, 3600.0)
+    r.prestart()
+    time.sleep(0.05)
+    assert drv.reconciles == [] and r._thread.is_alive()
+    r.start()
+    deadline = time.monotonic() + 2
+    while not drv.reconciles and time.monotonic() < deadline:
+        time.sleep(0.005)
+    assert drv.reconciles == [[]]
+    r.stop()
+    idle = ImplicitReconciler(0.0, 3600.0)
+    idle.prestart()
+    idle.stop()
+    idle._thread.join(1)
+    assert not idle._thread.is_alive() and drv.reconciles == [[]]
+
+
+def test_offer_processor_prestart_runs_no_cycle_before_start(drv):
+    """The loop thread exists before registration, but an offer-less cycle does nothing until the
+    processor is started; ``start`` after ``prestart`` keeps the one thread."""
+    c = Client()
+    p = processor(c, offer_wait_s=0.01)
+    p.prestart()
+    thread = p._thread
+    time.sleep(0.05)
+    assert c.received == [] and thread.is_alive()
+    p.start()
+    assert p._thread is thread
+    p.enqueue([offer("o1")])
+    deadline = time.monotonic() + 2
+    while not c.received and time.monotonic() < deadline:
+        time.sleep(0.005)
+    assert c.received == ["o1"]
+    p.stop()
+
+
 # ---------------------------------------------------------------------------------------
 # FrameworkScheduler callbacks
 
