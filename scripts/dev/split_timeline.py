@@ -26,7 +26,33 @@ ap.add_argument("--cycles", type=int, default=5)
 ap.add_argument("--agent0", choices=["process", "thread"], default="process",
                 help="agent 0 in a process of its own, or on a thread of the scheduler's process (as bench.py's "
                      "default)")
+ap.add_argument("--spans", default="",
+                help="comma-separated module:Qual.name callables to trace as spans (e.g. "
+                     "dcos_commons_amd.http.server:ApiServer.start)")
 args = ap.parse_args()
+
+
+def _wrap_spans(spec: str) -> None:
+    import functools
+    import importlib
+
+    for item in filter(None, spec.split(",")):
+        mod_name, qual = item.split(":")
+        owner = importlib.import_module(mod_name)
+        parts = qual.split(".")
+        for p in parts[:-1]:
+            owner = getattr(owner, p)
+        raw = owner.__dict__.get(parts[-1]) if isinstance(owner, type) else getattr(owner, parts[-1])
+        fn = raw.__func__ if isinstance(raw, (staticmethod, classmethod)) else raw
+
+        def make(fn=fn, name=parts[-1] if parts[-1] != "__init__" else parts[-2]):
+            @functools.wraps(fn)
+            def w(*a, **k):
+                with trace.span(name, "dev"):
+                    return fn(*a, **k)
+            return w
+        w = make()
+        setattr(owner, parts[-1], type(raw)(w) if isinstance(raw, (staticmethod, classmethod)) else w)
 
 proc, ports = MP.spawn()
 client = MP.MasterClient("127.0.0.1", ports["control"])
@@ -68,6 +94,7 @@ def _run(self, *a, **k):
 
 
 DB.SchedulerRunner.run = _run
+_wrap_spans(args.spans)
 b = DB.DeployBench(args.n, master_client=client)
 for _ in range(3):
     b.run_cycle()
