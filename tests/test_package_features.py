@@ -347,6 +347,29 @@ def test_hdfs_everything_on():
             assert r.get_task_config(pod, "node", name)
 
 
+def test_cassandra_everything_on():
+    """TLS, password authentication with authorization, secure JMX, G1 and metrics together: every
+    template of the node pod renders and the pod's secrets are merged under one ``secrets`` key."""
+    import yaml
+    r = (test_cassandra.runner().set_options(
+        "service.security.transport_encryption.enabled", "true",
+        "service.security.authentication.enabled", "true",
+        "service.security.authentication.superuser.password_secret_path", "c/su",
+        "service.security.authorization.enabled", "true",
+        "service.jmx.enabled", "true", "service.jmx.password_file", "c/pw", "service.jmx.access_file", "c/acc",
+        "service.jmx.key_store", "c/ks", "service.jmx.key_store_password_file", "c/ksp",
+        "nodes.heap.gc", "G1", "cassandra.metrics_enabled", "true")
+        .set_scheduler_env(DCOS_SERVICE_ACCOUNT_CREDENTIAL=CRED).run())
+    task = r.service_spec.pod("node").task("server")
+    names = {c.name for c in task.config_files}
+    assert names == {"cassandra", "rackdc", "jvm", "metrics-reporter", "cqlshrc", "jmx-ssl-setup"}
+    for name in names:
+        assert r.get_task_config("node", "server", name)
+    cfg = yaml.safe_load(r.get_task_config("node", "server", "cassandra"))
+    assert cfg["client_encryption_options"]["enabled"] is True and cfg["authorizer"] == "CassandraAuthorizer"
+    assert len(r.service_spec.pod("node").secrets) == 5 and [t.name for t in task.transport_encryption] == ["node"]
+
+
 # -- helloworld ----------------------------------------------------------------------------------
 def _hello(spec="svc.yml"):
     return ServiceTestRunner.for_framework("helloworld", spec).set_scheduler_env(SDK_REVIVE_INTERVAL_S="0")
