@@ -33,6 +33,7 @@ from .process_exit import ProcessExit
 
 LOGGER = logging.getLogger(__name__)
 TWO_WEEK_SEC = 2 * 7 * 24 * 60 * 60
+API_SERVER_WAIT_S = 5.0   # SDK_EARLY_SUBSCRIBE: how long early offers wait for the API server
 Cap = P.FrameworkInfo.Capability
 
 
@@ -115,21 +116,36 @@ class FrameworkRunner:
                                                                 self.scheduler_config)
         from dcos_commons_amd.http.server import ApiServer
 
-        self.api_server = ApiServer.start(self.scheduler_config, client.get_http_endpoints(),
-                                          self.framework_scheduler.set_api_server_started,
-                                          scheduler_hostname=hostname)
+        def start_api_server():
+            self.api_server = ApiServer.start(self.scheduler_config, client.get_http_endpoints(),
+                                              self.framework_scheduler.set_api_server_started,
+                                              scheduler_hostname=hostname)
+
+        early = self.scheduler_config.is_early_subscribe()
+        if not early:
+            start_api_server()
         info = self.get_framework_info(framework_store.fetch_framework_id())
         factory = self.driver_factory or self._default_driver_factory()
         self.driver = factory(self.framework_scheduler, info)
         prestart = self.scheduler_config.thread_prestart()
         if prestart == "before" or (prestart == "after" and block):
             self.framework_scheduler.prestart()
-        if not block:
+        if early:
+            # SUBSCRIBE goes out first and the API server starts during the registration round
+            # trip; offers that arrive before it is up wait for it instead of being declined
+            self.framework_scheduler.api_server_wait_s = API_SERVER_WAIT_S
             self.driver.start()
+            start_api_server()
+        if not block:
+            if not early:
+                self.driver.start()
             if prestart == "after":
                 self.framework_scheduler.prestart()
             return self.driver
-        self.driver.run()
+        if early:
+            self.driver.join()
+        else:
+            self.driver.run()
         self.api_server.join()
         ProcessExit.exit(ProcessExit.DRIVER_EXITED)
         return None

@@ -79,6 +79,7 @@ class FrameworkScheduler:
         self.implicit_reconciler = implicit_reconciler
         self._register_called = False
         self._api_server_started = threading.Event()
+        self.api_server_wait_s = 0.0    # offers before the API server is up: declined (0) or held
         self._lock = threading.Lock()
 
     # -- configuration ---------------------------------------------------------------
@@ -159,7 +160,7 @@ class FrameworkScheduler:
         trace.instant("offers_in", "driver", n=len(offers))
         try:
             metrics.increment_received_offers(len(offers))
-            if not self._api_server_started.is_set():
+            if not self._api_server_started.is_set() and not self._api_server_started.wait(self.api_server_wait_s):
                 LOGGER.info("Declining %d offer%s: Waiting for API server to start.", len(offers),
                             "" if len(offers) == 1 else "s")
                 decline_short(offers)

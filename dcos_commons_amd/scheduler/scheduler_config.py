@@ -320,6 +320,12 @@ class SchedulerConfig:
         v = self.env.get_optional("SDK_THREAD_PRESTART", "false").strip().lower()
         return {"true": "before", "1": "before", "0": "false", "no": "false"}.get(v, v)
 
+    def is_early_subscribe(self) -> bool:
+        """Send SUBSCRIBE before starting the API server, which then starts during the registration
+        round trip (``SDK_EARLY_SUBSCRIBE``; ``FrameworkRunner.start``). The reference starts the
+        server first and declines offers that arrive before it is up."""
+        return self.env.get_optional_boolean("SDK_EARLY_SUBSCRIBE", False)
+
     def offer_hold_s(self) -> float:
         """Hold unused offers this long while WORKING instead of declining them for 1 h
         (0 = reference behaviour: long decline + rate-limited revive)."""
