@@ -182,3 +182,22 @@ def test_bench_inprocess_topology():
     rec = _json_lines(p.stdout)[0]
     _check(rec, 2, 1, 0)
     assert "topology" not in rec["config"]
+
+
+@pytest.mark.parametrize("env", [{"SDK_EARLY_SUBSCRIBE": "true"}, {"SDK_THREAD_PRESTART": "before"},
+                                 {"SDK_THREAD_PRESTART": "after", "SDK_EARLY_SUBSCRIBE": "true"}])
+def test_startup_order_flags_deploy_and_recover(monkeypatch, env):
+    """SUBSCRIBE before the API server (early offers wait for it) and the offer-loop threads created
+    ahead of registration: a deploy, a restart and a replace still complete, and no offer was
+    declined for want of the API server."""
+    from dcos_commons_amd.benchmarks.deploy_bench import DeployBench
+    from dcos_commons_amd.framework import framework_scheduler as FS
+
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    declined = []
+    orig = FS.decline_short
+    monkeypatch.setattr(FS, "decline_short", lambda offers, *a, **k: (declined.extend(offers), orig(offers, *a, **k)))
+    r = DeployBench(1, timeout_s=20, allocation_interval_s=0.05).run_cycle()
+    assert r.deploy_s > 0 and r.mttr_restart_s > 0 and r.mttr_replace_s > 0
+    assert declined == []
