@@ -323,7 +323,8 @@ class SchedulerConfig:
     def is_early_subscribe(self) -> bool:
         """Send SUBSCRIBE before starting the API server, which then starts during the registration
         round trip (``SDK_EARLY_SUBSCRIBE``; ``FrameworkRunner.start``). The reference starts the
-        server first and declines offers that arrive before it is up."""
+        server first and declines offers that arrive before it is up. Not adopted: no difference on
+        the box (1 pod 2.01 vs 2.02 ms; profiles/early_subscribe_ab_r06_box.txt)."""
         return self.env.get_optional_boolean("SDK_EARLY_SUBSCRIBE", False)
 
     def offer_hold_s(self) -> float:
