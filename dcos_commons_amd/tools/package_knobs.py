@@ -5,10 +5,11 @@ Each knob is one setting of the application's own configuration file -- a ``cass
 (Cassandra 3.11) or an ``hdfs-site.xml`` / ``core-site.xml`` property (Hadoop 2.x) -- with its type
 and the application's default. From a table the generator writes, between marker lines:
 
-* the package option (``universe/config.json``: ``cassandra.<key>`` / ``hdfs.<key>`` with type,
-  default and description),
+* the package option (``universe/config.json``: ``cassandra.<key>``, or for hdfs the reference
+  package's own option path -- ``name_node.<key>``, ``data_node.<key>``, ``hdfs.<key>`` -- with
+  type, default and description),
 * the scheduler environment entry that carries it to every task (``marathon.json.mustache``:
-  ``"TASKCFG_ALL_<ENV>": "{{cassandra.<key>}}"``; the scheduler's TaskEnvRouter hands
+  ``"TASKCFG_ALL_<ENV>": "{{<option path>}}"``; the scheduler's TaskEnvRouter hands
   ``TASKCFG_ALL_*`` to every pod without the prefix),
 * the line of the config template that consumes it (``cassandra.yaml``: ``<key>: {{<ENV>}}``,
   ``hdfs-site.xml``: ``<property><name>..</name><value>{{<ENV>}}</value></property>``). A knob whose
@@ -36,7 +37,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)
 
 
 class Knob(NamedTuple):
-    key: str                 # option key under the package section, and (upper-cased) the env name
+    key: str                 # option key under the package section (cassandra) or full option path (hdfs)
     setting: str             # the application's own name for it
     type: str                # JSON schema type: integer | number | boolean | string
     default: object
