@@ -179,6 +179,17 @@ def cluster_request(method: str, cluster_path: str, retry: bool = True, raise_on
                 status, body = 404, {"message": f"no such metrics endpoint: {path}"}
         elif path == "/dcos-metadata/dcos-version.json":
             body = {"version": c.dcos_version, "dcos-variant": "open"}
+        elif path.startswith("/ca/") and c.dcos is None:
+            status, body = 404, {"message": "no cluster CA: the stand-in runs without dcos_security"}
+        elif path == "/ca/dcos-ca.crt" and m == "GET":
+            # the CA bundle is served as PEM, not JSON
+            return Response(200, c.dcos.root_cert.encode("utf-8"), {"Content-Type": "application/x-pem-file"}, path)
+        elif path == "/ca/api/v2/sign" and m == "POST":
+            data, _ = _body(kwargs)
+            status, body = c.dcos.sign(json.loads(data or b"{}"))
+        elif path == "/ca/api/v2/bundle" and m == "POST":
+            data, _ = _body(kwargs)
+            status, body = c.dcos.bundle(json.loads(data or b"{}"))
         elif path.startswith("/marathon/v2/groups"):
             gid = path[len("/marathon/v2/groups"):].split("?")[0]
             if m == "GET":
@@ -418,6 +429,19 @@ def service_task_exec(service_name: Optional[str], task_name: str, cmd: str) -> 
     """``dcos task exec <task> <cmd>``: runs in the task's sandbox with its environment."""
     tid = _find_task_id(service_name, task_name)
     return _cluster().task_exec(tid, cmd)
+
+
+def marathon_task_sandbox(task_name: str) -> str:
+    """The sandbox directory of the Marathon task (scheduler) named ``task_name``."""
+    from dcos_commons_amd.testing.cluster import scheduler_task_prefix
+
+    c = _cluster()
+    for app_id in c.marathon.app_ids():
+        if scheduler_task_prefix(app_id).startswith(task_name) or app_id.strip("/") == task_name.strip("/"):
+            sandbox = c.marathon.sandbox(app_id)
+            if sandbox is not None:
+                return sandbox
+    raise KeyError(f"no marathon task {task_name} with a sandbox")
 
 
 def marathon_task_exec(task_name: str, cmd: str, print_output: bool = True) -> Tuple[int, str, str]:
