@@ -31,8 +31,10 @@ def test_accepts_follow_their_record_in_order_and_coalesce():
     assert log == [("record", ["a1", "a2"]), ("send", ["a1", "a2"]),
                    ("record", ["b", "c", "d"]), ("send", ["b"]), ("send", ["c"]), ("send", ["d"])]
     assert p.writes == 2
+    writer = p._thread
     p.close()
-    assert not any(t.name == "launch-writer" for t in threading.enumerate())
+    # this pipeline's writer ended (other tests' schedulers may still own writers of that name)
+    assert writer is not None and not writer.is_alive()
 
 
 def test_failed_record_drops_the_operations():
