@@ -781,3 +781,4 @@ def test_pipelined_launch_whose_record_fails_is_dropped(env):
     persister.set_many = failing_set_many
     resp = hh.scheduler.offers([offer_for_a()], launch_stream=sent.append)
     assert sent == [] and resp.recommendations == []   # the offer is left unused (declined by the cycle)
+    hh.scheduler.close()                               # ends the pipeline's writer thread
