@@ -110,8 +110,10 @@ def main(argv=None) -> int:
     if world > 1:
         import torch.distributed as dist
 
+        # auto: RCCL with one rank per GPU; more ranks than GPUs (a one-GPU rehearsal) cannot share a
+        # device under RCCL ("Duplicate GPU detected"), so they use gloo
         backend = args.dist_backend if args.dist_backend != "auto" else (
-            "nccl" if torch.cuda.is_available() else "gloo")
+            "nccl" if torch.cuda.is_available() and world <= torch.cuda.device_count() else "gloo")
         args.dist_backend = backend
         if torch.cuda.is_available():
             # one rank per GPU; more ranks than GPUs share them round-robin (gloo rehearsals)
