@@ -128,6 +128,11 @@ def test_cassandra_authentication_and_authorization(tmp_path):
     assert any("ALTER ROLE cassandra" in l and "SUPERUSER = false" in l for l in lines)
     alters = [l for l in lines if "ALTER KEYSPACE system_auth" in l]
     assert len(alters) == 2 and all(l.startswith("-u admin -p s3cret") for l in alters)
+    # the schema backup logs in the same way
+    (sandbox / "container-path" / "snapshot").mkdir(parents=True)
+    backup = pod.task("backup-schema").command.value.replace("{{CASSANDRA_VERSION}}", "3.11.6")
+    subprocess.run(["bash", "-c", backup], cwd=sandbox, env=dict(env, POD_INSTANCE_INDEX="0"), check=True)
+    assert log.read_text().splitlines()[-1].startswith("-u admin -p s3cret -e DESC SCHEMA")
 
 
 def test_cassandra_marathon_health_check_rlimits_and_profile():
