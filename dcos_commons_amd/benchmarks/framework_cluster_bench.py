@@ -15,7 +15,7 @@ reference's unchanged packages (``testing.cluster.reference_packages``: its ``un
   other two nodes too, so they learn the new seed address).
 * hdfs (3 journal, 2 name + zkfc, 3 data): deploy, timed the same way; then an ``hdfs-site.xml``
   change (``TASKCFG_ALL_CLIENT_READ_SHORTCIRCUIT_STREAMS_CACHE_EXPIRY_MS`` + 1, the reference's
-  ``test_modify_app_config``; a package without that option gets its name-node handler count + 1): Marathon restarts the scheduler and its ``update`` plan relaunches
+  ``test_modify_app_config``; both package sets carry it): Marathon restarts the scheduler and its ``update`` plan relaunches
   every node. ``update_s`` is timed from the new scheduler's SUBSCRIBE to the plan answering 200
   with every node relaunched; ``update_total_s`` from the Marathon update (it includes starting the
   scheduler process).
@@ -44,8 +44,7 @@ FINISH_TASKS = ("-init_system_keyspaces", "-format", "-bootstrap", "-zkfc-format
 HDFS_TASKS = 10
 HDFS_OPTIONS = {"journal_node": {"readiness_check": {"delay": 0, "interval": 1}},
                 "data_node": {"readiness_check": {"delay": 0, "interval": 1}}}
-APP_CONFIG_FIELDS = ("TASKCFG_ALL_CLIENT_READ_SHORTCIRCUIT_STREAMS_CACHE_EXPIRY_MS",   # the reference's test
-                     "TASKCFG_ALL_HDFS_NAME_NODE_HANDLER_COUNT")
+APP_CONFIG_FIELDS = ("TASKCFG_ALL_CLIENT_READ_SHORTCIRCUIT_STREAMS_CACHE_EXPIRY_MS",)   # the reference's test
 
 
 class _Watch:
